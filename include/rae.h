@@ -1,0 +1,155 @@
+/*
+ * rae.h -- C ABI of the MI355X-native relation-autoencoder training path.
+ *
+ * This is the drop-in boundary for the reference's compiled Theano function
+ *
+ *   self.func['train'] = theano.function(inputs=[batch_index, neg1, neg2], outputs=cost,
+ *                                        updates=..., givens={xFeats, ents_1, ents_2})
+ *        (learning/OieInduction.py:146-149, called at :189)
+ *   self.func['label_<split>'] = theano.function(inputs=[batch_index],
+ *                                        outputs=(labels, probs), ...)
+ *        (learning/OieInduction.py:151-155, called at :245,259,337)
+ *
+ * and for the model/optimizer objects that function is built from
+ * (OieModelFunctions learning/OieModel.py:16-101, AdaGrad/SGD learning/Optimizers.py:6-52).
+ *
+ * Conventions
+ *  - plain C types only; every pointer named *_dev is a device pointer (HBM, gfx950);
+ *  - the caller owns all parameter / accumulator / data / exchange memory (they are
+ *    Theano shared variables in the reference: learning/OieInduction.py:439-449,
+ *    learning/Optimizers.py:12-15); the plan holds borrowed pointers plus a private
+ *    workspace allocated once in rae_plan_create;
+ *  - every call returns 0 on success and a negative RAE_E* code on error;
+ *    rae_last_error() returns a thread-local message for the last failure;
+ *  - hot calls (rae_step_*, rae_train_step, rae_label) never allocate or synchronise, so
+ *    they can be captured into a HIP graph; they are stream-ordered on `stream`;
+ *  - a plan is single-caller (like a Theano function); different plans may run on
+ *    different streams concurrently.
+ */
+#ifndef RAE_H
+#define RAE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* rae_stream_t;   /* == hipStream_t */
+
+#define RAE_OK 0
+#define RAE_E_INVALID (-1)     /* bad argument / unsupported configuration           */
+#define RAE_E_HIP (-2)         /* HIP runtime error                                  */
+#define RAE_E_OVERFLOW (-3)    /* a per-step row-index partition overflowed its LDS  */
+#define RAE_E_STATE (-4)       /* call sequence error                                */
+
+/* decoder type: learning/models/decoders/Decoder.py:84-93 ('sp', 'rescal', 'rescal+sp') */
+#define RAE_DEC_SP 0
+#define RAE_DEC_RESCAL 1
+#define RAE_DEC_HYBRID 2
+
+/* optimizer: learning/OieInduction.py:261-269 ('adagrad', 'sgd') */
+#define RAE_OPT_ADAGRAD 0
+#define RAE_OPT_SGD 1
+
+/* negative-sample column addressing */
+#define RAE_NEG_PER_CALL 0     /* neg arrays are (s, l_global): column = example-in-batch */
+#define RAE_NEG_PER_EPOCH 1    /* neg arrays are (s, N): column = global example index     */
+
+typedef struct rae_config {
+    int32_t decoder;          /* RAE_DEC_*                                                */
+    int32_t optimizer;        /* RAE_OPT_*                                                */
+    int64_t n_examples;       /* N: rows of the train split (learning/OieData.py:78)     */
+    int64_t n_features;       /* d: feature dimensionality (OieData.py:96-98)             */
+    int64_t n_entities;       /* n: entity vocabulary (OieData.py:92-94)                  */
+    int32_t relations;        /* m = K (--relations, OieInduction.py:469)                 */
+    int32_t embed;            /* r (--embed-size, :468)                                   */
+    int32_t neg_samples;      /* s (--neg-samples, :470)                                  */
+    int32_t batch_size;       /* l: examples per rank per step (--batch-size, :467)       */
+    int32_t world_size;       /* data-parallel ranks G (1 = single GPU)                   */
+    int32_t rank;             /* this rank                                                */
+    float learning_rate;      /* --learning-rate (:466)                                   */
+    float alpha;              /* entropy scale (--alpha, :479; OieModel.py:81)            */
+    float lambda1;            /* --l1 (:471)                                              */
+    float lambda2;            /* --l2 (:472)                                              */
+    int32_t ext_reg;          /* --ext-reg (:477; OieModel.py:60-62)                      */
+    int32_t max_batch_nnz;    /* max nnz over global batches (sizes the W row index)      */
+    int32_t max_row_nnz;      /* max nnz of one example row                               */
+    int32_t neg_mode;         /* RAE_NEG_*                                                */
+    int64_t neg_stride;       /* row stride (elements) of the neg arrays                  */
+} rae_config;
+
+/* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
+ *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]
+ *   (RelationClassifier.py:24-25, OieModel.py:105, SelectionalPreferences.py:13-19,
+ *    Bilinear.py:14-17, BilinearPlusSP.py:14-23), acc_* the AdaGrad accumulators of the
+ *   same shapes (Optimizers.py:12-15; unused for SGD, may be NULL).
+ * data: the train split CSR (OieData.py:83-90) + entity ids.  values may be NULL
+ *   (binary features: every stored value is 1.0, OieData.py:88).
+ * exchange: per-example records of the global batch, rae_exchange_floats() floats; rank k
+ *   writes rows [k*l, (k+1)*l); between rae_step_forward and rae_step_update the caller
+ *   all-gathers it across ranks (no-op for world_size == 1).
+ * costs: one float per batch index (the value func['train'] returns).
+ */
+typedef struct rae_buffers {
+    float* W; float* Wb; float* A; float* Ab;
+    float* C1; float* C2; float* R3;             /* R3 = R (rescal) or C (hybrid) */
+    float* acc_W; float* acc_Wb; float* acc_A; float* acc_Ab;
+    float* acc_C1; float* acc_C2; float* acc_R3;
+    const int32_t* indptr; const int32_t* indices; const float* values;
+    const int32_t* args1; const int32_t* args2;
+    const int32_t* neg1; const int32_t* neg2;   /* may be NULL until rae_set_negatives */
+    float* exchange;
+    float* costs;
+} rae_buffers;
+
+typedef struct rae_plan rae_plan;
+
+/* --- lifetime ---------------------------------------------------------------------- */
+int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, rae_plan** out);
+int rae_plan_destroy(rae_plan* plan);
+const char* rae_last_error(void);
+int rae_version(void);
+
+/* floats per example record and per global batch in the exchange buffer */
+int64_t rae_exchange_record_floats(const rae_config* cfg);
+int64_t rae_exchange_floats(const rae_config* cfg);
+
+/* --- negatives --------------------------------------------------------------------- */
+/* Point the plan at negative-sample arrays (learning/NegativeExampleGenerator.py:14-32
+ * output, int32).  mode RAE_NEG_PER_EPOCH: (s, N) arrays for the whole epoch
+ * (OieInduction.py:183-184); RAE_NEG_PER_CALL: (s, l_global) arrays of one batch
+ * (OieInduction.py:187-189). */
+int rae_set_negatives(rae_plan* plan, const int32_t* neg1_dev, const int32_t* neg2_dev,
+                      int32_t mode, int64_t stride);
+
+/* --- the training step (func['train']) --------------------------------------------- */
+/* Batch addressed as  batch = *cursor + step_offset  (cursor: device int64 owned by the
+ * plan) so a captured sequence of steps can be replayed for successive batches.        */
+int rae_set_cursor(rae_plan* plan, int64_t batch, rae_stream_t stream);
+int rae_advance_cursor(rae_plan* plan, int64_t count, rae_stream_t stream);
+/* K1: per-example encoder + decoder forward/backward of this rank's l examples, plus the
+ * per-step row index of the global batch.  Writes the exchange records.                  */
+int rae_step_forward(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
+/* K2 (+K3 when lambda1/lambda2 != 0): deterministic per-row gradient reduction over the
+ * global batch and the optimizer update of every parameter; writes costs[batch].        */
+int rae_step_update(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
+/* One whole func['train'](batch_index, neg1, neg2) call on a single rank:
+ * rae_set_negatives(PER_CALL) + forward + update for `batch_index`.                    */
+int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,
+                   const int32_t* neg2_dev, rae_stream_t stream);
+/* Device error word (overflow flags); host reads it with rae_check(). */
+int rae_check(rae_plan* plan);
+
+/* --- labelling (func['label_<split>'], RelationClassifier.py:39-48) ----------------- */
+/* rows [row0, row0+nrows) of any CSR split with the current W/Wb: labels = argmax(S)
+ * (int64, first max) and probs = softmax(S) (fp32, may be NULL).                        */
+int rae_label(const int32_t* indptr, const int32_t* indices, const float* values,
+              const float* W, const float* Wb, int32_t relations, int64_t row0,
+              int64_t nrows, int64_t* labels_out, float* probs_out, rae_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAE_H */

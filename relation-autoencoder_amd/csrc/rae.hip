@@ -1,0 +1,523 @@
+// MI355X (gfx950) relation-autoencoder training path: kernels + C ABI (include/rae.h).
+//
+// Per training step (one func['train'] call of learning/OieInduction.py:189):
+//   k_forward  grid = HA + HW index workgroups + l example workgroups
+//              index WGs : per-step row index of the global batch (rae_index.hpp)
+//              example WG: encoder + decoder forward/backward of one example (rae_sp.hpp,
+//                          rae_bilinear.hpp) -> exchange record
+//   [caller all-gathers the exchange records across data-parallel ranks]
+//   k_update   one wavefront per distinct referenced row / dense decoder row / bias:
+//              deterministic gradient sums + AdaGrad/SGD in place (rae_update.hpp)
+//   k_dense_w + k_finalize_cost   only when lambda1/lambda2 != 0 (dense W regulariser)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/rae.h"
+#include "rae_bilinear.hpp"
+#include "rae_common.hpp"
+#include "rae_index.hpp"
+#include "rae_sp.hpp"
+#include "rae_step.hpp"
+#include "rae_update.hpp"
+
+using namespace rae;
+
+#define RAE_VERSION 1
+
+// ======================================================================================
+// kernels
+// ======================================================================================
+template <int DEC, bool V4>
+__global__ __launch_bounds__(RAE_BT) void k_forward(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t g = *a.cursor + a.step_offset;
+    const int bid = blockIdx.x;
+    if (bid < a.HA) {
+        build_index_partition(a, g, true, bid, smem);
+        return;
+    }
+    if (bid < a.HA + a.HW) {
+        build_index_partition(a, g, false, bid - a.HA, smem);
+        return;
+    }
+    const int bl = bid - a.HA - a.HW;
+    if (DEC == RAE_DEC_SP) sp_example<V4, V4>(a, g, bl, smem);
+    else bilinear_example<V4>(a, g, bl, smem, DEC == RAE_DEC_HYBRID);
+}
+
+template <int OPT, bool V4>
+__global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    const int nw = gridDim.x * RAE_NWAVE;
+    const int64_t g = *a.cursor + a.step_offset;
+    const int64_t ex0 = g * (int64_t)a.L;
+    const int TA = total_rows(a.hdrA, a.HA);
+    const int TW = total_rows(a.hdrW, a.HW);
+    const int nC = (a.dec != RAE_DEC_RESCAL) ? 2 * a.r : 0;
+    const int nR = (a.dec != RAE_DEC_SP) ? a.r * a.r : 0;
+    const int T = nC + TA + TW + nR + 1;
+    for (int t = gw; t < T; t += nw) {
+        int tt = t;
+        if (tt < nC) {
+            task_sp_matrix_row<OPT>(a, tt / a.r, tt % a.r, tt, lane);
+            continue;
+        }
+        tt -= nC;
+        if (tt < TA) {
+            int u;
+            const int h = locate_row(a.hdrA, a.HA, tt, &u);
+            task_entity_row<OPT, V4>(a, h, u, lane);
+            continue;
+        }
+        tt -= TA;
+        if (tt < TW) {
+            int u;
+            const int h = locate_row(a.hdrW, a.HW, tt, &u);
+            task_feature_row<OPT, V4>(a, ex0, h, u, lane);
+            continue;
+        }
+        tt -= TW;
+        if (tt < nR) {
+            task_bilinear_row<OPT>(a, tt, nC + tt, lane);
+            continue;
+        }
+        task_bias_and_cost<OPT>(a, ex0, lane);
+    }
+}
+
+// Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,
+// reset the scratch, L1/L2 partials of the old W per block (fixed grid -> deterministic).
+template <int OPT>
+__global__ __launch_bounds__(RAE_BT) void k_dense_w(StepArgs a) {
+    __shared__ double red[2 * RAE_NWAVE];
+    const int64_t total = a.d * (int64_t)a.m;
+    double l1 = 0.0, l2 = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)RAE_BT + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * RAE_BT) {
+        const float w = a.W[i];
+        const float gg = a.gWs[i] + a.l1adj * sgnf(w) + 2.f * a.l2adj * w;
+        a.gWs[i] = 0.f;
+        l1 += fabsf(w);
+        l2 += (double)w * w;
+        float ac = (OPT == 0) ? a.aW[i] : 0.f;
+        a.W[i] = opt_update<OPT>(w, &ac, gg, a.lr);
+        if (OPT == 0) a.aW[i] = ac;
+    }
+    l1 = wave_sum_d(l1);
+    l2 = wave_sum_d(l2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * w] = l1;
+        red[2 * w + 1] = l2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int i = 0; i < RAE_NWAVE; ++i) {
+            s1 += red[2 * i];
+            s2 += red[2 * i + 1];
+        }
+        const int slot = a.nregC + blockIdx.x;
+        a.regpart[2 * slot] = s1;
+        a.regpart[2 * slot + 1] = s2;
+    }
+}
+
+// cost = base + lambda1*adjust*L1 + lambda2*adjust*L2   (learning/OieInduction.py:134-135)
+__global__ void k_finalize_cost(StepArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double L1 = 0.0, L2 = 0.0;
+    if (a.ext_reg)
+        for (int i = 0; i < a.nregC; ++i) {
+            L1 += a.regpart[2 * i];
+            L2 += a.regpart[2 * i + 1];
+        }
+    for (int i = 0; i < a.nregW; ++i) {
+        L1 += a.regpart[2 * (a.nregC + i)];
+        L2 += a.regpart[2 * (a.nregC + i) + 1];
+    }
+    const int64_t batch = *a.cursor + a.step_offset;
+    a.costs[batch] = (float)((double)*a.base_cost + (double)a.l1adj * L1 + (double)a.l2adj * L2);
+}
+
+__global__ void k_add_cursor(int64_t* cursor, int64_t count) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *cursor += count;
+}
+__global__ void k_set_cursor(int64_t* cursor, int64_t v) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *cursor = v;
+}
+
+// func['label_*']: labels = argmax(S) (first max), probs = softmax(S); one wave per example
+// (RelationClassifier.py:39-48).
+__global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* indptr, const int32_t* indices,
+                                                  const float* values, const float* W,
+                                                  const float* Wb, int m, int64_t row0,
+                                                  int64_t nrows, int64_t* labels, float* probs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * RAE_NWAVE;
+    for (int64_t e = blockIdx.x * (int64_t)RAE_NWAVE + (threadIdx.x >> 6); e < nrows; e += nw) {
+        const int64_t ex = row0 + e;
+        const int p0 = indptr[ex], p1 = indptr[ex + 1];
+        float S[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) S[cc] = 0.f;
+        for (int p = p0; p < p1; ++p) {
+            const int64_t f = indices[p];
+            const float v = values ? values[p] : 1.f;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const int k = lane + 64 * cc;
+                if (k < m) S[cc] += v * W[f * m + k];
+            }
+        }
+        float best = -INFINITY;
+        int bk = 0x7fffffff;
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+            const int k = lane + 64 * cc;
+            if (k < m) {
+                S[cc] += Wb[k];
+                if (S[cc] > best) { best = S[cc]; bk = k; }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int ok = __shfl_xor(bk, o, 64);
+            if (ob > best || (ob == best && ok < bk)) { best = ob; bk = ok; }
+        }
+        if (lane == 0) labels[e] = bk;
+        if (probs) {
+            float se = 0.f;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const int k = lane + 64 * cc;
+                if (k < m) se += expf(S[cc] - best);
+            }
+            se = wave_sum(se);
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const int k = lane + 64 * cc;
+                if (k < m) probs[e * m + k] = expf(S[cc] - best) / se;
+            }
+        }
+    }
+}
+
+// ======================================================================================
+// host side / C ABI
+// ======================================================================================
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess)                                                              \
+            return fail(RAE_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+struct rae_plan {
+    rae_config cfg;
+    rae_buffers buf;
+    StepArgs args;
+    int64_t* d_cursor = nullptr;
+    int64_t* d_zero = nullptr;
+    int* d_err = nullptr;
+    char* ws = nullptr;
+    size_t smem_fwd = 0;
+    int grid_fwd = 0, grid_update = 0, grid_dense = 0;
+    bool v4 = false;
+};
+
+extern "C" const char* rae_last_error(void) { return g_last_error.c_str(); }
+extern "C" int rae_version(void) { return RAE_VERSION; }
+
+extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
+    if (!cfg) return -1;
+    return make_layout(cfg->decoder, cfg->relations, cfg->embed, cfg->neg_samples).rec;
+}
+extern "C" int64_t rae_exchange_floats(const rae_config* cfg) {
+    if (!cfg) return -1;
+    return rae_exchange_record_floats(cfg) * (int64_t)cfg->batch_size * cfg->world_size;
+}
+
+static int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, rae_plan** out) {
+    if (!cfg || !buf || !out) return fail(RAE_E_INVALID, "null argument");
+    const rae_config& c = *cfg;
+    if (c.decoder < 0 || c.decoder > 2) return fail(RAE_E_INVALID, "decoder must be 0..2");
+    if (c.optimizer < 0 || c.optimizer > 1) return fail(RAE_E_INVALID, "optimizer must be 0..1");
+    if (c.relations < 1 || c.relations > 1024)
+        return fail(RAE_E_INVALID, "relations must be in [1, 1024]");
+    if (c.embed < 1 || c.embed > 1024) return fail(RAE_E_INVALID, "embed must be in [1, 1024]");
+    if (c.neg_samples < 1) return fail(RAE_E_INVALID, "neg_samples must be >= 1");
+    if (c.batch_size < 1 || c.world_size < 1 || c.rank < 0 || c.rank >= c.world_size)
+        return fail(RAE_E_INVALID, "bad batch_size/world_size/rank");
+    if (c.n_examples < (int64_t)c.batch_size * c.world_size)
+        return fail(RAE_E_INVALID, "fewer examples than one global batch");
+    if (c.n_entities < 1 || c.n_features < 1 || c.n_entities >= (1ll << 31))
+        return fail(RAE_E_INVALID, "bad n_entities / n_features");
+    if (!buf->W || !buf->Wb || !buf->A || !buf->Ab || !buf->indptr || !buf->indices ||
+        !buf->args1 || !buf->args2 || !buf->exchange || !buf->costs)
+        return fail(RAE_E_INVALID, "missing required buffer");
+    if (c.decoder != RAE_DEC_RESCAL && (!buf->C1 || !buf->C2))
+        return fail(RAE_E_INVALID, "C1/C2 required for this decoder");
+    if (c.decoder != RAE_DEC_SP && !buf->R3) return fail(RAE_E_INVALID, "R/C tensor required");
+    if (c.optimizer == RAE_OPT_ADAGRAD &&
+        (!buf->acc_W || !buf->acc_Wb || !buf->acc_A || !buf->acc_Ab ||
+         (c.decoder != RAE_DEC_RESCAL && (!buf->acc_C1 || !buf->acc_C2)) ||
+         (c.decoder != RAE_DEC_SP && !buf->acc_R3)))
+        return fail(RAE_E_INVALID, "AdaGrad accumulators required");
+
+    rae_plan* p = new rae_plan();
+    p->cfg = c;
+    p->buf = *buf;
+    StepArgs& a = p->args;
+    memset(&a, 0, sizeof(a));
+    const int L = c.batch_size * c.world_size;
+    const int NJ = 2 + 2 * c.neg_samples;
+    a.dec = c.decoder;
+    a.opt = c.optimizer;
+    a.N = c.n_examples;
+    a.d = c.n_features;
+    a.n = c.n_entities;
+    a.m = c.relations;
+    a.r = c.embed;
+    a.s = c.neg_samples;
+    a.l = c.batch_size;
+    a.L = L;
+    a.rank = c.rank;
+    a.lr = c.learning_rate;
+    a.alpha = c.alpha;
+    // adjust = batch / N_train (learning/OieInduction.py:131) with the GLOBAL batch
+    const double adjust = (double)L / (double)c.n_examples;
+    a.l1adj = (float)(c.lambda1 * adjust);
+    a.l2adj = (float)(c.lambda2 * adjust);
+    a.invD = (float)(1.0 / (4.0 * L + 2.0 * L * c.neg_samples));
+    a.ext_reg = c.ext_reg;
+    a.reg_on = (c.lambda1 != 0.f || c.lambda2 != 0.f) ? 1 : 0;
+    a.indptr = buf->indptr;
+    a.indices = buf->indices;
+    a.values = buf->values;
+    a.args1 = buf->args1;
+    a.args2 = buf->args2;
+    a.neg1 = buf->neg1;
+    a.neg2 = buf->neg2;
+    a.neg_mode = c.neg_mode;
+    a.neg_stride = c.neg_stride;
+    a.W = buf->W; a.Wb = buf->Wb; a.A = buf->A; a.Ab = buf->Ab;
+    a.C1 = buf->C1; a.C2 = buf->C2; a.R3 = buf->R3;
+    a.aW = buf->acc_W; a.aWb = buf->acc_Wb; a.aA = buf->acc_A; a.aAb = buf->acc_Ab;
+    a.aC1 = buf->acc_C1; a.aC2 = buf->acc_C2; a.aR3 = buf->acc_R3;
+    a.ex = buf->exchange;
+    a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples);
+    a.costs = buf->costs;
+    p->v4 = (c.relations % 4 == 0) && (c.embed % 4 == 0);
+
+    // row-index partitions: ~1024 records per partition on average, LDS holds RAE_KCAP
+    a.RA = L * NJ;
+    a.RW = c.max_batch_nnz > 0 ? c.max_batch_nnz : 1;
+    a.HA = ceil_div(a.RA, 1024);
+    a.HW = ceil_div(a.RW, 1024);
+    int bbits = 1;
+    while ((1 << bbits) < L) ++bbits;
+    a.posbits = 31 - bbits;
+    if (c.max_row_nnz >= (1 << a.posbits)) {
+        delete p;
+        return fail(RAE_E_INVALID, "an example has too many features for the record encoding");
+    }
+    // parameter / dense-row partial slots for the regulariser
+    a.nregC = (c.decoder != RAE_DEC_RESCAL ? 2 * c.embed : 0) +
+              (c.decoder != RAE_DEC_SP ? c.embed * c.embed : 0);
+    p->grid_dense = 1024;
+    a.nregW = a.reg_on ? p->grid_dense : 0;
+
+    // workspace
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~size_t(255);
+        return o;
+    };
+    const size_t o_cursor = take(8), o_zero = take(8), o_err = take(8), o_base = take(8);
+    const size_t o_hdrA = take(8 * a.HA), o_hdrW = take(8 * a.HW);
+    const size_t o_srecA = take(4ull * a.HA * a.RA), o_urowA = take(4ull * a.HA * a.RA),
+                 o_ustA = take(4ull * a.HA * a.RA);
+    const size_t o_srecW = take(4ull * a.HW * a.RW), o_urowW = take(4ull * a.HW * a.RW),
+                 o_ustW = take(4ull * a.HW * a.RW);
+    const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
+    const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
+    hipError_t e = hipMalloc(&p->ws, off);
+    if (e != hipSuccess) {
+        delete p;
+        return fail(RAE_E_HIP, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
+    }
+    (void)hipMemset(p->ws, 0, off);
+    p->d_cursor = reinterpret_cast<int64_t*>(p->ws + o_cursor);
+    p->d_zero = reinterpret_cast<int64_t*>(p->ws + o_zero);
+    p->d_err = reinterpret_cast<int*>(p->ws + o_err);
+    a.base_cost = reinterpret_cast<float*>(p->ws + o_base);
+    a.hdrA = reinterpret_cast<int32_t*>(p->ws + o_hdrA);
+    a.hdrW = reinterpret_cast<int32_t*>(p->ws + o_hdrW);
+    a.srecA = reinterpret_cast<int32_t*>(p->ws + o_srecA);
+    a.urowA = reinterpret_cast<int32_t*>(p->ws + o_urowA);
+    a.ustartA = reinterpret_cast<int32_t*>(p->ws + o_ustA);
+    a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
+    a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
+    a.ustartW = reinterpret_cast<int32_t*>(p->ws + o_ustW);
+    a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
+    a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
+    a.err = p->d_err;
+    a.cursor = p->d_cursor;
+
+    const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
+    const size_t smem_ex = 4ull * ex_floats;
+    const size_t smem_idx = 8ull * RAE_KCAP + 4ull * 16;
+    p->smem_fwd = smem_ex > smem_idx ? smem_ex : smem_idx;
+    if (p->smem_fwd > 160 * 1024) {
+        (void)hipFree(p->ws);
+        delete p;
+        return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
+    }
+    p->grid_fwd = a.HA + a.HW + c.batch_size;
+    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + 1;
+    int gu = ceil_div(tasks, RAE_NWAVE);
+    p->grid_update = gu < 1 ? 1 : (gu > 4096 ? 4096 : gu);
+    *out = p;
+    return RAE_OK;
+}
+
+extern "C" int rae_plan_destroy(rae_plan* p) {
+    if (!p) return RAE_OK;
+    if (p->ws) (void)hipFree(p->ws);
+    delete p;
+    return RAE_OK;
+}
+
+extern "C" int rae_set_negatives(rae_plan* p, const int32_t* n1, const int32_t* n2, int32_t mode,
+                                 int64_t stride) {
+    if (!p || !n1 || !n2) return fail(RAE_E_INVALID, "null argument");
+    if (mode != RAE_NEG_PER_CALL && mode != RAE_NEG_PER_EPOCH)
+        return fail(RAE_E_INVALID, "bad negatives mode");
+    p->args.neg1 = n1;
+    p->args.neg2 = n2;
+    p->args.neg_mode = mode;
+    p->args.neg_stride = stride;
+    return RAE_OK;
+}
+
+extern "C" int rae_set_cursor(rae_plan* p, int64_t batch, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    hipLaunchKernelGGL(k_set_cursor, dim3(1), dim3(64), 0, (hipStream_t)stream, p->d_cursor, batch);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    hipLaunchKernelGGL(k_add_cursor, dim3(1), dim3(64), 0, (hipStream_t)stream, p->d_cursor, count);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+
+template <int DEC>
+static void launch_fwd_dec(rae_plan* p, const StepArgs& a, hipStream_t st) {
+    if (p->v4)
+        hipLaunchKernelGGL((k_forward<DEC, true>), dim3(p->grid_fwd), dim3(RAE_BT), p->smem_fwd, st, a);
+    else
+        hipLaunchKernelGGL((k_forward<DEC, false>), dim3(p->grid_fwd), dim3(RAE_BT), p->smem_fwd, st, a);
+}
+
+static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
+    if (!p->args.neg1 || !p->args.neg2) return fail(RAE_E_STATE, "negatives not set");
+    StepArgs a = p->args;
+    a.cursor = cursor;
+    a.step_offset = off;
+    switch (a.dec) {
+        case RAE_DEC_SP: launch_fwd_dec<RAE_DEC_SP>(p, a, st); break;
+        case RAE_DEC_RESCAL: launch_fwd_dec<RAE_DEC_RESCAL>(p, a, st); break;
+        default: launch_fwd_dec<RAE_DEC_HYBRID>(p, a, st); break;
+    }
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+
+static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
+    StepArgs a = p->args;
+    a.cursor = cursor;
+    a.step_offset = off;
+    const dim3 gu(p->grid_update), bt(RAE_BT);
+    if (a.opt == RAE_OPT_ADAGRAD) {
+        if (p->v4) hipLaunchKernelGGL((k_update<0, true>), gu, bt, 0, st, a);
+        else hipLaunchKernelGGL((k_update<0, false>), gu, bt, 0, st, a);
+    } else {
+        if (p->v4) hipLaunchKernelGGL((k_update<1, true>), gu, bt, 0, st, a);
+        else hipLaunchKernelGGL((k_update<1, false>), gu, bt, 0, st, a);
+    }
+    HIPCHK(hipGetLastError());
+    if (a.reg_on) {
+        if (a.opt == RAE_OPT_ADAGRAD)
+            hipLaunchKernelGGL((k_dense_w<0>), dim3(p->grid_dense), bt, 0, st, a);
+        else
+            hipLaunchKernelGGL((k_dense_w<1>), dim3(p->grid_dense), bt, 0, st, a);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_finalize_cost, dim3(1), dim3(64), 0, st, a);
+        HIPCHK(hipGetLastError());
+    }
+    return RAE_OK;
+}
+
+extern "C" int rae_step_forward(rae_plan* p, int64_t off, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    return launch_forward(p, p->d_cursor, off, (hipStream_t)stream);
+}
+extern "C" int rae_step_update(rae_plan* p, int64_t off, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    return launch_update(p, p->d_cursor, off, (hipStream_t)stream);
+}
+
+extern "C" int rae_train_step(rae_plan* p, int64_t batch, const int32_t* n1, const int32_t* n2,
+                              rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (p->cfg.world_size != 1)
+        return fail(RAE_E_STATE, "rae_train_step is the single-rank func['train'] path");
+    const int64_t nb = p->cfg.n_examples / p->cfg.batch_size;
+    if (batch < 0 || batch >= nb) return fail(RAE_E_INVALID, "batch index out of range");
+    int rc = rae_set_negatives(p, n1, n2, RAE_NEG_PER_CALL, p->cfg.batch_size);
+    if (rc) return rc;
+    rc = launch_forward(p, p->d_zero, batch, (hipStream_t)stream);
+    if (rc) return rc;
+    return launch_update(p, p->d_zero, batch, (hipStream_t)stream);
+}
+
+extern "C" int rae_check(rae_plan* p) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    int e = 0;
+    HIPCHK(hipMemcpy(&e, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) return fail(RAE_E_OVERFLOW, "row-index partition overflowed its LDS capacity (flags=" +
+                                           std::to_string(e) + ")");
+    return RAE_OK;
+}
+
+extern "C" int rae_label(const int32_t* indptr, const int32_t* indices, const float* values,
+                         const float* W, const float* Wb, int32_t m, int64_t row0, int64_t nrows,
+                         int64_t* labels, float* probs, rae_stream_t stream) {
+    if (!indptr || !indices || !W || !Wb || !labels) return fail(RAE_E_INVALID, "null argument");
+    if (m < 1 || m > 512) return fail(RAE_E_INVALID, "relations must be in [1, 512] for labelling");
+    if (nrows <= 0) return RAE_OK;
+    int64_t blocks = (nrows + RAE_NWAVE - 1) / RAE_NWAVE;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_label, dim3((unsigned)blocks), dim3(RAE_BT), 0, (hipStream_t)stream, indptr,
+                       indices, values, W, Wb, m, row0, nrows, labels, probs);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}

@@ -1,0 +1,107 @@
+"""ctypes binding of the C ABI declared in include/rae.h (librae_hip.so).
+
+The product path has no CPU fallback: if the HIP library is missing or a call fails, an
+exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "librae_hip.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+RAE_OK = 0
+RAE_DEC = {"sp": 0, "rescal": 1, "rescal+sp": 2}
+RAE_OPT = {"adagrad": 0, "sgd": 1}
+RAE_NEG_PER_CALL = 0
+RAE_NEG_PER_EPOCH = 1
+
+# Every symbol include/rae.h declares (checked by tests/test_abi.py against the header).
+EXPORTS = (
+    "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version",
+    "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
+    "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
+    "rae_train_step", "rae_check", "rae_label",
+)
+
+
+class RaeConfig(C.Structure):
+    _fields_ = [
+        ("decoder", C.c_int32), ("optimizer", C.c_int32),
+        ("n_examples", C.c_int64), ("n_features", C.c_int64), ("n_entities", C.c_int64),
+        ("relations", C.c_int32), ("embed", C.c_int32), ("neg_samples", C.c_int32),
+        ("batch_size", C.c_int32), ("world_size", C.c_int32), ("rank", C.c_int32),
+        ("learning_rate", C.c_float), ("alpha", C.c_float), ("lambda1", C.c_float),
+        ("lambda2", C.c_float), ("ext_reg", C.c_int32), ("max_batch_nnz", C.c_int32),
+        ("max_row_nnz", C.c_int32), ("neg_mode", C.c_int32), ("neg_stride", C.c_int64),
+    ]
+
+
+_P = C.c_void_p
+
+
+class RaeBuffers(C.Structure):
+    _fields_ = [
+        ("W", _P), ("Wb", _P), ("A", _P), ("Ab", _P), ("C1", _P), ("C2", _P), ("R3", _P),
+        ("acc_W", _P), ("acc_Wb", _P), ("acc_A", _P), ("acc_Ab", _P), ("acc_C1", _P),
+        ("acc_C2", _P), ("acc_R3", _P),
+        ("indptr", _P), ("indices", _P), ("values", _P), ("args1", _P), ("args2", _P),
+        ("neg1", _P), ("neg2", _P), ("exchange", _P), ("costs", _P),
+    ]
+
+
+class RaeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load librae_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("RAE_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RaeError(f"{p} not found: build the HIP extension first "
+                       "(python __graft_entry__.py build)")
+    lib = C.CDLL(p)
+    lib.rae_last_error.restype = C.c_char_p
+    lib.rae_version.restype = C.c_int
+    lib.rae_exchange_record_floats.restype = C.c_int64
+    lib.rae_exchange_record_floats.argtypes = [C.POINTER(RaeConfig)]
+    lib.rae_exchange_floats.restype = C.c_int64
+    lib.rae_exchange_floats.argtypes = [C.POINTER(RaeConfig)]
+    lib.rae_plan_create.argtypes = [C.POINTER(RaeConfig), C.POINTER(RaeBuffers), C.POINTER(_P)]
+    lib.rae_plan_destroy.argtypes = [_P]
+    lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
+    lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]
+    lib.rae_advance_cursor.argtypes = [_P, C.c_int64, _P]
+    lib.rae_step_forward.argtypes = [_P, C.c_int64, _P]
+    lib.rae_step_update.argtypes = [_P, C.c_int64, _P]
+    lib.rae_train_step.argtypes = [_P, C.c_int64, _P, _P, _P]
+    lib.rae_check.argtypes = [_P]
+    lib.rae_label.argtypes = [_P, _P, _P, _P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, _P]
+    for fn in ("rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
+               "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
+               "rae_check", "rae_label"):
+        getattr(lib, fn).restype = C.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "rae call"):
+    if rc != RAE_OK:
+        msg = load().rae_last_error()
+        raise RaeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()

@@ -1,0 +1,233 @@
+"""The device training step behind ``func['train']`` and ``func['label_<split>']``.
+
+Owns the HBM-resident dataset arrays, the exchange and cost buffers, and the C-ABI plan
+(include/rae.h).  Two ways to drive it:
+
+* ``train_call(batch, neg1, neg2)`` -- exactly the reference's compiled function signature
+  (learning/OieInduction.py:146-149,189): host negatives for one batch in, cost out.
+* ``run(first_batch, count)`` -- many steps back to back on per-epoch negatives resident in
+  HBM, captured into HIP graphs (torch.cuda.CUDAGraph) so a step costs two kernel launches
+  and no host round trip; per-batch costs stay on the device until the epoch ends.
+
+Data-parallel: each rank computes its l examples of every global batch of L = G*l
+examples; ``exchange`` (dist.py) all-gathers the per-example records between the forward
+and the update kernels, so every rank applies the identical update.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .data import batch_nnz_stats
+
+
+class DeviceSplit:
+    """One split's CSR + entity ids in HBM (int32; values kept only if not all 1.0)."""
+
+    def __init__(self, split, device):
+        x = split.xFeats
+        self.N = int(x.shape[0])
+        self.d = int(x.shape[1])
+        self.indptr_np = np.asarray(x.indptr, dtype=np.int64)
+        if self.indptr_np[-1] >= 2 ** 31:
+            raise ValueError("nnz exceeds int32 CSR addressing")
+        self.indptr = torch.as_tensor(self.indptr_np.astype(np.int32), device=device)
+        self.indices = torch.as_tensor(np.asarray(x.indices, dtype=np.int32), device=device)
+        vals = np.asarray(x.data, dtype=np.float32)
+        self.values = None if (vals.size == 0 or np.all(vals == 1.0)) else \
+            torch.as_tensor(vals, device=device)
+        self.args1 = torch.as_tensor(split.args1, device=device)
+        self.args2 = torch.as_tensor(split.args2, device=device)
+
+
+class TrainEngine:
+    def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
+                 lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
+                 device=None):
+        self.lib = _lib.load()
+        self.model = model
+        self.device = device if device is not None else model.params[0].device
+        self.world_size = int(world_size)
+        self.rank = int(rank)
+        self.exchange = exchange
+        self.graph_chunk = int(graph_chunk)
+        dec = model.decoder
+        self.m, self.r, self.s, self.l = model.m, model.r, model.s, model.l
+        self.L = self.l * self.world_size
+        self.split = train_split if isinstance(train_split, DeviceSplit) else \
+            DeviceSplit(train_split, self.device)
+        self.N = self.split.N
+        self.nb = self.N // self.L                                     # OieInduction.py:98
+        mbn, mrn = batch_nnz_stats(self.split.indptr_np, self.L)
+        named = model.named_params()
+        acc = {}
+        if optimizer.accumulator is not None:
+            acc = dict(zip(model.param_names, optimizer.accumulator))
+        cfg = _lib.RaeConfig()
+        cfg.decoder = _lib.RAE_DEC[dec.model_type]
+        cfg.optimizer = _lib.RAE_OPT[optimizer.name]
+        cfg.n_examples = self.N
+        cfg.n_features = self.split.d
+        cfg.n_entities = model.n
+        cfg.relations = self.m
+        cfg.embed = self.r
+        cfg.neg_samples = self.s
+        cfg.batch_size = self.l
+        cfg.world_size = self.world_size
+        cfg.rank = self.rank
+        cfg.learning_rate = float(learning_rate)
+        cfg.alpha = float(model.alpha)
+        cfg.lambda1 = float(lambda1)
+        cfg.lambda2 = float(lambda2)
+        cfg.ext_reg = 1 if model.extended_reg else 0
+        cfg.max_batch_nnz = mbn
+        cfg.max_row_nnz = mrn
+        cfg.neg_mode = _lib.RAE_NEG_PER_EPOCH
+        cfg.neg_stride = self.N
+        self.cfg = cfg
+        self.rec_floats = int(self.lib.rae_exchange_record_floats(C.byref(cfg)))
+        self.exchange_buf = torch.zeros(int(self.lib.rae_exchange_floats(C.byref(cfg))),
+                                        dtype=torch.float32, device=self.device)
+        self.costs = torch.zeros(max(self.nb, 1), dtype=torch.float32, device=self.device)
+        # per-epoch negatives live in fixed buffers (captured graphs keep their pointers)
+        self.neg1 = torch.zeros((self.s, self.N), dtype=torch.int32, device=self.device)
+        self.neg2 = torch.zeros((self.s, self.N), dtype=torch.int32, device=self.device)
+        self.call_neg = torch.zeros((2, self.s, self.L), dtype=torch.int32, device=self.device)
+        R3 = named.get("R", named.get("C"))
+        bufs = _lib.RaeBuffers()
+        p = _lib.ptr
+        bufs.W, bufs.Wb, bufs.A, bufs.Ab = p(named["W"]), p(named["Wb"]), p(named["A"]), p(named["Ab"])
+        bufs.C1, bufs.C2, bufs.R3 = p(named.get("C1")), p(named.get("C2")), p(R3)
+        bufs.acc_W, bufs.acc_Wb = p(acc.get("W")), p(acc.get("Wb"))
+        bufs.acc_A, bufs.acc_Ab = p(acc.get("A")), p(acc.get("Ab"))
+        bufs.acc_C1, bufs.acc_C2 = p(acc.get("C1")), p(acc.get("C2"))
+        bufs.acc_R3 = p(acc.get("R", acc.get("C")))
+        bufs.indptr, bufs.indices = p(self.split.indptr), p(self.split.indices)
+        bufs.values = p(self.split.values)
+        bufs.args1, bufs.args2 = p(self.split.args1), p(self.split.args2)
+        bufs.neg1, bufs.neg2 = p(self.neg1), p(self.neg2)
+        bufs.exchange, bufs.costs = p(self.exchange_buf), p(self.costs)
+        self._bufs = bufs
+        self._keep = (named, acc, R3)
+        handle = C.c_void_p()
+        _lib.check(self.lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(handle)),
+                   "rae_plan_create")
+        self.plan = handle
+        self._graphs = {}
+        self._epoch_mode = None
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "plan", None):
+            self._graphs.clear()
+            self.lib.rae_plan_destroy(self.plan)
+            self.plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self):
+        _lib.check(self.lib.rae_check(self.plan), "rae_check")
+
+    # ------------------------------------------------------------------ func['train']
+    def train_call(self, batch_index, neg1, neg2) -> float:
+        """One ``func['train'](batch_index, neg1, neg2)`` call (OieInduction.py:146-149):
+        neg1/neg2 are (s, l) int32 host arrays; returns the batch cost as a Python float."""
+        if self.world_size != 1:
+            raise RuntimeError("train_call is the single-rank func['train'] path")
+        n1 = np.ascontiguousarray(neg1, dtype=np.int32)
+        n2 = np.ascontiguousarray(neg2, dtype=np.int32)
+        if n1.shape != (self.s, self.l) or n2.shape != (self.s, self.l):
+            raise ValueError(f"neg arrays must be ({self.s}, {self.l}), got {n1.shape}, {n2.shape}")
+        b = int(batch_index)
+        if not 0 <= b < self.nb:
+            raise IndexError(f"batch index {b} out of range [0, {self.nb})")
+        self.call_neg[0].copy_(torch.from_numpy(n1))
+        self.call_neg[1].copy_(torch.from_numpy(n2))
+        st = self._stream()
+        _lib.check(self.lib.rae_train_step(self.plan, b, C.c_void_p(self.call_neg[0].data_ptr()),
+                                           C.c_void_p(self.call_neg[1].data_ptr()), st),
+                   "rae_train_step")
+        self._epoch_mode = None
+        cost = float(self.costs[b].item())
+        self.check()
+        return cost
+
+    # ------------------------------------------------------------------ epoch path
+    def set_epoch_negatives(self, neg1, neg2):
+        """(s, N) negatives of one epoch (OieInduction.py:183-184), host or device."""
+        self.neg1.copy_(torch.as_tensor(np.asarray(neg1, dtype=np.int32)) if not
+                        torch.is_tensor(neg1) else neg1)
+        self.neg2.copy_(torch.as_tensor(np.asarray(neg2, dtype=np.int32)) if not
+                        torch.is_tensor(neg2) else neg2)
+        self._ensure_epoch_mode()
+
+    def _ensure_epoch_mode(self):
+        if self._epoch_mode is not True:
+            _lib.check(self.lib.rae_set_negatives(self.plan, C.c_void_p(self.neg1.data_ptr()),
+                                                  C.c_void_p(self.neg2.data_ptr()),
+                                                  _lib.RAE_NEG_PER_EPOCH, self.N),
+                       "rae_set_negatives")
+            self._epoch_mode = True
+
+    def _steps_eager(self, count, st):
+        for i in range(count):
+            _lib.check(self.lib.rae_step_forward(self.plan, i, st), "rae_step_forward")
+            if self.exchange is not None:
+                self.exchange(self.exchange_buf)
+            _lib.check(self.lib.rae_step_update(self.plan, i, st), "rae_step_update")
+        _lib.check(self.lib.rae_advance_cursor(self.plan, count, st), "rae_advance_cursor")
+
+    def _graph(self, count):
+        g = self._graphs.get(count)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.graph(g, stream=s):
+                self._steps_eager(count, self._stream())
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._graphs[count] = g
+        return g
+
+    def run(self, first_batch: int, count: int, graph: bool = True):
+        """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
+        negatives; costs land in self.costs[first_batch:first_batch+count]."""
+        self._ensure_epoch_mode()
+        st = self._stream()
+        _lib.check(self.lib.rae_set_cursor(self.plan, int(first_batch), st), "rae_set_cursor")
+        if not graph or self.graph_chunk <= 1:
+            self._steps_eager(count, st)
+            return
+        T = self.graph_chunk
+        full, rem = divmod(int(count), T)
+        if full:
+            g = self._graph(T)
+            for _ in range(full):
+                g.replay()
+        if rem:
+            self._steps_eager(rem, self._stream())
+
+    # ------------------------------------------------------------------ labelling
+    def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):
+        """labels (int64) and probs (fp32) of rows [row0, row0+nrows) of a split with the
+        current W/Wb (RelationClassifier.py:39-48)."""
+        lab = torch.empty(nrows, dtype=torch.int64, device=self.device)
+        pr = torch.empty((nrows, self.m), dtype=torch.float32, device=self.device) if probs else None
+        W, Wb = self.model.params[0], self.model.params[1]
+        _lib.check(self.lib.rae_label(
+            C.c_void_p(split.indptr.data_ptr()), C.c_void_p(split.indices.data_ptr()),
+            C.c_void_p(split.values.data_ptr()) if split.values is not None else None,
+            C.c_void_p(W.data_ptr()), C.c_void_p(Wb.data_ptr()), self.m, int(row0), int(nrows),
+            C.c_void_p(lab.data_ptr()), C.c_void_p(pr.data_ptr()) if pr is not None else None,
+            self._stream()), "rae_label")
+        return lab, pr

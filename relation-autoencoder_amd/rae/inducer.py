@@ -1,0 +1,247 @@
+"""ReconstructInducer: the trainer that drives the training path
+(learning/OieInduction.py:26-319), same constructor, same ``func`` dictionary, same epoch
+loop and RNG consumption -- with the step running on MI355X.
+"""
+from __future__ import annotations
+
+import sys
+import time
+from collections import Counter
+
+import numpy as np
+import torch
+
+from .data import SPLIT_LABELS
+from .engine import DeviceSplit, TrainEngine
+from .evaluation import construct_split_evaluator
+from .model import OieModelFunctions, _as_bool, make_optimizer
+from .negatives import NegativeExampleGenerator
+
+
+class _TrainFunction:
+    """``func['train'](batch_index, neg1, neg2) -> cost`` (OieInduction.py:146-149)."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def __call__(self, batch_index, neg1, neg2):
+        return self.engine.train_call(batch_index, neg1, neg2)
+
+
+class _LabelFunction:
+    """``func['label_<split>'](batch_index) -> (labels, probs)`` (OieInduction.py:151-155)."""
+
+    def __init__(self, engine, split, batch_size):
+        self.engine = engine
+        self.split = split
+        self.l = batch_size
+
+    def __call__(self, batch_index):
+        b = int(batch_index)
+        lab, pr = self.engine.label(self.split, b * self.l, self.l)
+        return lab.cpu().numpy(), pr.cpu().numpy()
+
+    def all_labels(self, nb_batches):
+        """Labels of the first nb_batches*l rows in one launch (tail dropped as the
+        reference's per-batch loop does, OieInduction.py:337)."""
+        lab, _ = self.engine.label(self.split, 0, nb_batches * self.l, probs=False)
+        return lab.cpu().numpy()
+
+
+class ReconstructInducer:
+    def __init__(self, data, gold_standard, rng, nb_epochs, learning_rate, batch_size,
+                 embed_size, nb_relations, nb_neg_samples, lambda1, lambda2, optimization,
+                 model_name, decoder_model, external_embeddings, extended_regularizer,
+                 frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
+                 graph_chunk=64):
+        self.data = data
+        self.goldStandard = gold_standard
+        self.rng = rng
+        self.nb_epochs = nb_epochs
+        self.learningRate = learning_rate
+        self.batch_size = batch_size
+        self.embedSize = embed_size
+        self.relationNum = nb_relations
+        self.neg_sample_num = nb_neg_samples
+        self.lambdaL1 = lambda1
+        self.lambdaL2 = lambda2
+        self.optimization = optimization
+        self.modelName = model_name
+        self.decoder_type = decoder_model
+        self.extEmb = external_embeddings
+        self.extendedReg = extended_regularizer
+        self.frequentEval = _as_bool(frequent_eval)
+        self.alpha = alpha
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.world_size = int(world_size)
+        self.rank = int(rank)
+        self.exchange = exchange
+        self.graph_chunk = graph_chunk
+        self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
+        self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
+                        f"_embedsize{embed_size}_l1{lambda1}_l2{lambda2}_opt{optimization}"
+                        f"_rel_num{nb_relations}_batch{batch_size}_negs{nb_neg_samples}")
+        self.modelFunc = OieModelFunctions(rng, embed_size, nb_relations, nb_neg_samples,
+                                           batch_size, decoder_model, data, extended_regularizer,
+                                           alpha, external_embeddings=external_embeddings,
+                                           device=self.device)          # :90
+        self.func = dict(zip([SPLIT_LABELS[0]] + ["label_" + s for s in SPLIT_LABELS],
+                             [None] * (1 + len(SPLIT_LABELS))))         # :91
+        self.cur_epoch = 0
+        self.evaluator = {s: None for s in SPLIT_LABELS}
+        for split in self.data.generate_split_keys():
+            self.evaluator[split] = construct_split_evaluator(
+                (gold_standard or {}).get(split, {}), split)
+        self.batch_reps = {s: None for s in SPLIT_LABELS}
+        for split in self.data.generate_split_keys():
+            # Py2 integer division: tail dropped (:98); data-parallel global batch
+            self.batch_reps[split] = self.data.split[split].args1.shape[0] // (
+                self.batch_size * (self.world_size if split == "train" else 1))
+        self.cluster = {s: None for s in SPLIT_LABELS}
+        self.train_errors = []
+        self.epoch_costs = []
+        self.engine = None
+        self.optimizer = None
+
+    def initialize(self):
+        """OieInduction.py:103-108: re-draw all parameters from the shared RNG."""
+        self._drop_engine()
+        self.modelFunc = OieModelFunctions(self.rng, self.embedSize, self.relationNum,
+                                           self.neg_sample_num, self.batch_size,
+                                           self.decoder_type, self.data, self.extendedReg,
+                                           self.alpha, external_embeddings=self.extEmb,
+                                           device=self.device)
+
+    def _drop_engine(self):
+        if self.engine is not None:
+            self.engine.close()
+        self.engine = None
+        self.func = {k: None for k in self.func}
+
+    # ------------------------------------------------------------------ compile
+    def compile_function(self):
+        """OieInduction.py:118-155: build the train function and one labelling function
+        per split."""
+        self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)   # :137
+        self.engine = TrainEngine(self.modelFunc, self.optimizer, self.data.split["train"],
+                                  learning_rate=self.learningRate, lambda1=self.lambdaL1,
+                                  lambda2=self.lambdaL2, world_size=self.world_size,
+                                  rank=self.rank, exchange=self.exchange,
+                                  graph_chunk=self.graph_chunk, device=self.device)
+        self.func["train"] = _TrainFunction(self.engine)
+        for key in self.data.generate_split_keys():
+            ds = self.engine.split if key == "train" else DeviceSplit(self.data.split[key], self.device)
+            self.func["label_" + key] = _LabelFunction(self.engine, ds, self.batch_size)
+
+    def _check_for_compiled_functions(self):
+        return self.func.get("train") is not None
+
+    # ------------------------------------------------------------------ train / learn
+    def train(self, debug=False):
+        """OieInduction.py:157-170 (wall-clock timers instead of process CPU time)."""
+        t0 = time.perf_counter()
+        if not self._check_for_compiled_functions():
+            self.compile_function()
+        compile_duration = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        self.learn(debug=debug)
+        train_duration = time.perf_counter() - t0
+        print("Compiling completed in {:.1f}s".format(compile_duration), file=sys.stderr)
+        print("Training completed in {:.1f}s".format(train_duration), file=sys.stderr)
+        if self.cur_epoch:
+            print("Trained for {} epochs. Avg epoch duration: {:.1f}s".format(
+                self.cur_epoch, train_duration / float(self.cur_epoch)))
+
+    def draw_epoch_negatives(self):
+        """OieInduction.py:183-184: neg1 then neg2, each (s, N), from the shared RNG."""
+        N = self.data.split["train"].args1.shape[0]
+        neg1 = self.negativeSampler.get_negative_samples(N, self.neg_sample_num)
+        neg2 = self.negativeSampler.get_negative_samples(N, self.neg_sample_num)
+        return neg1, neg2
+
+    def learn(self, debug=False, verbose=True):
+        """OieInduction.py:172-219.  Per epoch: draw negatives on the host RNG (parity mode),
+        upload once, run every batch on the device, read the per-batch costs back and sum
+        them in batch order (err += cost, :189)."""
+        if not self._check_for_compiled_functions():
+            self.compile_function()
+        nb = self.batch_reps["train"]
+        epoch = 0
+        while epoch < self.nb_epochs:
+            t0 = time.perf_counter()
+            epoch += 1
+            self.cur_epoch = epoch
+            neg1, neg2 = self.draw_epoch_negatives()
+            self.engine.set_epoch_negatives(neg1, neg2)
+            if self.frequentEval:
+                # per-batch evaluation needs the host between batches (:190-198)
+                for b in range(nb):
+                    self.engine.run(b, 1, graph=False)
+                    if self._mode() == 1:
+                        print(b * self.batch_size, b, "#" * 60)
+                        print(self.get_clusters_size(), "\n")
+            else:
+                self.engine.run(0, nb)
+            costs = self.engine.costs[:nb].double().cpu().numpy()
+            self.engine.check()
+            self.epoch_costs.append(costs)
+            err = 0.0
+            for c in costs:
+                err += float(np.float32(c))
+            self.train_errors.append(err)
+            if verbose:
+                print("\nEPOCH", epoch)
+                print("Training error: {:.4f}".format(err))
+                print("Epoch duration: {:.1f}s".format(time.perf_counter() - t0))
+            if self._mode() == 1:
+                self.cluster["train"] = self.get_clusters_sets("train")
+                self._evaluate("train", verbose=verbose)
+            else:
+                for split in SPLIT_LABELS[1:]:
+                    self.cluster[split] = self.get_clusters_sets(split)
+                    self._evaluate(split, verbose=verbose)
+        return self.train_errors
+
+    # ------------------------------------------------------------------ clusters / eval
+    def _labels(self, split):
+        nbs = self.data.split[split].args1.shape[0] // self.batch_size
+        return self.func["label_" + split].all_labels(nbs)
+
+    def get_clusters_sets(self, split):
+        """get_clusters_sets (OieInduction.py:321-340): cluster id -> set of example ids."""
+        clusters = {i: set() for i in range(self.relationNum)}
+        for idx, pred in enumerate(self._labels(split)):
+            clusters[int(pred)].add(idx)
+        return clusters
+
+    def get_clusters_size(self, split="train"):
+        """get_clusters_size (OieInduction.py:248-259)."""
+        return Counter(int(x) for x in self._labels(split))
+
+    def _evaluate(self, split, verbose=True):
+        ev = self.evaluator.get(split)
+        if ev is None:
+            return None
+        ev.feed_induced_clusters(self.cluster[split])
+        f1, pre, rec = ev.compute_metrics()
+        if verbose:
+            print("{} f1: {:.4f} pre: {:.4f} rec: {:.4f}".format(split, f1, pre, rec))
+        return f1, pre, rec
+
+    def _mode(self):
+        """OieInduction.py:300-312."""
+        if len(self.data.split) == 1 and "train" in self.data.split:
+            return 1
+        if len(self.data.split) == 3 and all(k in self.data.split for k in SPLIT_LABELS):
+            return 2
+        raise Exception("Either 'train' split or 'train', 'valid' and 'test' splits should be defined")
+
+    def state_dict(self):
+        """Parameters + AdaGrad accumulators + RNG state (the reference's save() drops the
+        accumulators, OieInduction.py:110-116)."""
+        sd = {"params": {k: v.detach().cpu() for k, v in self.modelFunc.named_params().items()},
+              "rng": self.rng.get_state(), "epoch": self.cur_epoch}
+        if self.optimizer is not None and self.optimizer.accumulator is not None:
+            sd["acc"] = {k: v.detach().cpu() for k, v in
+                         zip(self.modelFunc.param_names, self.optimizer.accumulator)}
+        return sd

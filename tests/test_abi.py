@@ -1,0 +1,48 @@
+"""The C-ABI library builds, loads without a GPU and exports every symbol include/rae.h
+declares; the host-only entry points work."""
+import ctypes as C
+import os
+import re
+
+from conftest import ROOT
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "rae.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rae_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_header_declares_what_binding_expects():
+    from rae import _lib
+    assert header_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(built_lib):
+    for sym in header_symbols():
+        assert hasattr(built_lib, sym), sym
+
+
+def test_struct_layout_matches_header(built_lib):
+    from rae import _lib
+    cfg = _lib.RaeConfig()
+    cfg.decoder, cfg.relations, cfg.embed, cfg.neg_samples = 0, 100, 200, 20
+    cfg.batch_size, cfg.world_size = 100, 1
+    # record layout: P, dS (m) + V1, V2, dw1, dw2 (r) + coef 3*(2+2s) + loss, 16-B aligned
+    rec = built_lib.rae_exchange_record_floats(C.byref(cfg))
+    assert rec == ((2 * 100 + 4 * 200 + ((3 * 42 + 3) & ~3) + 1 + 3) & ~3)
+    assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 100
+    cfg.world_size = 8
+    assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 800
+    assert built_lib.rae_version() >= 1
+
+
+def test_plan_create_rejects_bad_config(built_lib):
+    from rae import _lib
+    cfg = _lib.RaeConfig()
+    cfg.decoder = 7
+    bufs = _lib.RaeBuffers()
+    h = C.c_void_p()
+    rc = built_lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(h))
+    assert rc == -1
+    assert b"decoder" in built_lib.rae_last_error()

@@ -1,0 +1,167 @@
+"""HIP training path vs the oracle / the reference's golden vectors (needs an MI355X).
+
+Tolerances (fp32 device arithmetic vs the float64 reference, Theano's default floatX):
+  per-batch cost        |dc| <= 2e-5 * max(1, |c|)
+  parameters            |dp| <= 2e-4 + 2e-3*|p|   after whole training runs
+  labels                identical wherever the reference's top-2 score margin > 1e-5
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import rae_oracle as O
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+COST_RTOL = 2e-5
+
+
+def _case(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    X = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(int(z["N"]), int(z["d"])))
+    return z, X
+
+
+def _inducer(z, X, dev, **kw):
+    from rae.data import DatasetManager, DatasetSplit
+    from rae.inducer import ReconstructInducer
+    data = DatasetManager({"train": DatasetSplit(z["args1"], z["args2"], X)}, z["freqs"],
+                          int(z["d"]))
+    assert np.array_equal(data.negSamplingCum, z["cum"])
+    rng = np.random.RandomState(int(z["seed"]))
+    ind = ReconstructInducer(data, {"train": {}}, rng, int(z["epochs"]), float(z["lr"]),
+                             int(z["l"]), int(z["r"]), int(z["m"]), int(z["s"]), float(z["l1"]),
+                             float(z["l2"]), str(z["optimizer"]), "golden", str(z["decoder"]),
+                             False, bool(int(z["ext_reg"])), False, float(z["alpha"]),
+                             device=dev, **kw)
+    return ind
+
+
+def _params(ind):
+    return {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
+
+
+def _assert_params_close(got, want, what):
+    for k in want:
+        err = np.abs(got[k] - want[k])
+        tol = 2e-4 + 2e-3 * np.abs(want[k])
+        assert np.all(err <= tol), f"{what} {k}: max err {err.max():.3e}"
+
+
+SP_CASES = ["sp_basic", "sp_reg", "sp_sgd_noext"]
+
+
+@pytest.mark.parametrize("name", SP_CASES)
+@pytest.mark.parametrize("graph", [True, False])
+def test_epoch_path_matches_reference_golden(built_lib, cuda_dev, name, graph):
+    z, X = _case(name)
+    ind = _inducer(z, X, cuda_dev, graph_chunk=2 if graph else 1)
+    for k, v in _params(ind).items():                     # init on the shared RNG
+        assert np.array_equal(v, z["init_" + k].astype(np.float32).astype(np.float64)), k
+    errs = ind.learn(verbose=False)
+    np.testing.assert_allclose(errs, z["errs"], rtol=COST_RTOL * 3, atol=0)
+    _assert_params_close(_params(ind), {k: z["final_" + k] for k in _params(ind)}, name)
+    lab = ind.func["label_train"].all_labels(ind.batch_reps["train"])
+    _assert_labels(lab, z, X)
+
+
+def _assert_labels(lab, z, X):
+    nrow = lab.shape[0]
+    S = np.asarray(X[:nrow] @ z["final_W"]) + z["final_Wb"]
+    srt = np.sort(S, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-5
+    assert np.array_equal(lab[clear], z["labels"][:nrow][clear])
+
+
+@pytest.mark.parametrize("name", SP_CASES)
+def test_func_train_per_call_matches_reference_golden(built_lib, cuda_dev, name):
+    """The reference's own call pattern: err += func['train'](b, neg1[:, cols], neg2[:, cols])."""
+    z, X = _case(name)
+    ind = _inducer(z, X, cuda_dev)
+    ind.compile_function()
+    l, nb = int(z["l"]), int(z["N"]) // int(z["l"])
+    for ep in range(int(z["epochs"])):
+        n1, n2 = z[f"neg1_e{ep}"], z[f"neg2_e{ep}"]
+        for b in range(nb):
+            c = ind.func["train"](b, n1[:, b * l:(b + 1) * l], n2[:, b * l:(b + 1) * l])
+            want = z["costs"][ep, b]
+            assert abs(c - want) <= COST_RTOL * max(1.0, abs(want)), (ep, b, c, want)
+    _assert_params_close(_params(ind), {k: z["final_" + k] for k in _params(ind)}, name)
+    labels, probs = ind.func["label_train"](0)
+    np.testing.assert_allclose(probs, z["probs"][:l], rtol=0, atol=2e-5)
+
+
+def _oracle_trajectory(decoder, data, seed, m, r, s, l, epochs, **hp):
+    tr = O.OracleTrainer(decoder, data.split["train"].xFeats, data.split["train"].args1,
+                         data.split["train"].args2, data.negSamplingCum,
+                         np.random.RandomState(seed), m, r, s, l, **hp)
+    costs = [tr.epoch()[0] for _ in range(epochs)]
+    return tr, np.array(costs)
+
+
+@pytest.mark.parametrize("shape", [
+    dict(N=400, d=300, m=8, r=16, s=4, l=50, ntrue=4),
+    dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10),   # headline K/r/s/l
+    dict(N=240, d=500, m=30, r=100, s=10, l=60, ntrue=6),       # config 2 K/r/s
+    dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5),          # non-multiple-of-4 (scalar path)
+])
+def test_synthetic_vs_oracle(built_lib, cuda_dev, shape):
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    data, gold = synthetic_dataset(shape["N"], shape["d"], shape["ntrue"], seed=99)
+    m, r, s, l = shape["m"], shape["r"], shape["s"], shape["l"]
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "syn", "sp", False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=2)
+    errs = ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory("sp", data, 2, m, r, s, l, 2, lr=0.1, alpha=1.0)
+    got = np.array(ind.epoch_costs)
+    np.testing.assert_allclose(got, costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "synthetic")
+
+
+def test_bitwise_deterministic(built_lib, cuda_dev):
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    out = []
+    for _ in range(2):
+        data, gold = synthetic_dataset(500, 900, 5, seed=7)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 50, 24, 12, 5,
+                                 0.0, 0.0, "adagrad", "det", "sp", False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=4)
+        ind.learn(verbose=False)
+        out.append(_params(ind))
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k]), k
+
+
+def test_label_pass_matches_oracle(built_lib, cuda_dev):
+    import torch
+    from rae.engine import DeviceSplit
+    from rae.data import synthetic_dataset
+    data, _ = synthetic_dataset(3000, 4000, 8, seed=5)
+    g = np.random.RandomState(0)
+    m = 100
+    W = g.standard_normal((4000, m)).astype(np.float32)
+    Wb = g.standard_normal(m).astype(np.float32)
+    split = DeviceSplit(data.split["train"], cuda_dev)
+    lab = torch.empty(3000, dtype=torch.int64, device=cuda_dev)
+    pr = torch.empty((3000, m), dtype=torch.float32, device=cuda_dev)
+    import ctypes as C
+    from rae import _lib
+    lib = _lib.load()
+    Wt, Wbt = torch.as_tensor(W, device=cuda_dev), torch.as_tensor(Wb, device=cuda_dev)
+    _lib.check(lib.rae_label(C.c_void_p(split.indptr.data_ptr()), C.c_void_p(split.indices.data_ptr()),
+                             None, C.c_void_p(Wt.data_ptr()), C.c_void_p(Wbt.data_ptr()), m, 0, 3000,
+                             C.c_void_p(lab.data_ptr()), C.c_void_p(pr.data_ptr()), None))
+    torch.cuda.synchronize()
+    want_lab, want_p = O.label(data.split["train"].xFeats, W.astype(np.float64), Wb.astype(np.float64))
+    S = np.asarray(data.split["train"].xFeats @ W.astype(np.float64)) + Wb
+    srt = np.sort(S, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert np.array_equal(lab.cpu().numpy()[clear], want_lab[clear])
+    np.testing.assert_allclose(pr.cpu().numpy(), want_p, rtol=1e-4, atol=1e-6)
