@@ -1,0 +1,228 @@
+"""Benchmark: train examples/sec (fwd+bwd+update) of the relation-VAE training step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--batch-size 100]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+A "step" is one func['train'] call on one global batch (l examples per rank): encoder +
+decoder forward/backward + AdaGrad update of every parameter.  Inputs (dataset, per-epoch
+negatives) are resident in HBM before the timed region; negative sampling (host RNG, as in
+the reference) is timed separately.  K steps are timed between barrier+synchronize pairs,
+max over ranks; value = K * global_batch / seconds (whole job).  Rank 0 prints one JSON line.
+
+Also reported: the forward kernel's roofline (algorithmic bytes per launch / its average
+duration from HIP events on the launch stream) and the CPU baseline -- the float64 numpy
+restatement of the reference's dense Theano schedule (oracle/rae_oracle.py) timed on a
+bounded sample of the same workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "relation-autoencoder_amd"))
+
+METRIC = "train examples/sec (fwd+bwd) K=100 d=200 neg=20 at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# BASELINE.json configs: N triples, feature dim, K, embed, neg, decoder
+CONFIGS = {
+    "c2": dict(N=100_000, d=2 ** 17, m=30, r=100, s=10, dec="sp", ntrue=30,
+               name="C2 synthetic 100k triples K=30 embed=100 neg=10 sp"),
+    "c3": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="sp", ntrue=100,
+               name="C3 synthetic 1M triples K=100 embed=200 neg=20 sp (headline)"),
+    "c4": dict(N=10_000_000, d=2 ** 20, m=300, r=300, s=50, dec="sp", ntrue=300,
+               name="C4 synthetic 10M triples K=300 embed=300 neg=50 sp"),
+    "c5": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="rescal", ntrue=100,
+               name="C5 synthetic 1M triples K=100 embed=200 neg=20 rescal"),
+}
+
+
+def forward_bytes(indptr, ex0, L, m, r, s, rec_floats, dec):
+    """Algorithmic HBM bytes of one forward launch over examples [ex0, ex0+L):
+    per example: CSR indptr+indices 4(f+1), W rows 4*f*m, entity/neg ids + Ab 8(2+2s),
+    A rows 4*r*(1+2s) (SP reads A[e1] and the negatives; RESCAL also A[e2]),
+    exchange record 4*rec; per launch: C1, C2 4*2*r*m, Wb 4m, the row index written
+    (3 int32 per record).  No cross-example reuse credited."""
+    f = np.diff(indptr[ex0:ex0 + L + 1]).astype(np.int64)
+    nrows = (1 + 2 * s) if dec == "sp" else (2 + 2 * s)
+    per_ex = 4 * (f + 1) + 4 * f * m + 8 * (2 + 2 * s) + 4 * r * nrows + 4 * rec_floats
+    per_launch = 4 * 2 * r * m + 4 * m + 12 * (L * (2 + 2 * s) + int(f.sum()))
+    return int(per_ex.sum() + per_launch)
+
+
+def cpu_baseline(data, cfg, l, budget_s, seed=2):
+    """Dense-schedule float64 oracle step on this host (one thread), bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rae_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=1)
+    except Exception:                                  # pragma: no cover
+        limiter = None
+    sp_ = data.split["train"]
+    rng = np.random.RandomState(seed)
+    p = O.init_params(rng, cfg["dec"], data.get_dimensionality(), cfg["m"],
+                      data.get_arg_voc_size(), cfg["r"])
+    acc = {k: np.zeros_like(v) for k, v in p.items()}
+    cum = data.negSamplingCum
+    steps, t_used = 0, 0.0
+    while t_used < budget_s or steps < 2:
+        b = steps
+        rows = slice(b * l, (b + 1) * l)
+        n1 = O.negative_samples(rng, cum, l, cfg["s"])
+        n2 = O.negative_samples(rng, cum, l, cfg["s"])
+        t0 = time.perf_counter()
+        res = O.train_step_grads(cfg["dec"], p, sp_.xFeats[rows], sp_.args1[rows],
+                                 sp_.args2[rows], n1, n2, alpha=1.0)
+        O.adagrad_apply(p, acc, res.grads, 0.1)
+        t_used += time.perf_counter() - t0
+        steps += 1
+        if steps >= 200:
+            break
+    if limiter is not None:
+        limiter.unregister() if hasattr(limiter, "unregister") else None
+    return dict(value=steps * l / t_used, unit="examples/s", cores=1, kind="port",
+                sample=f"{steps} dense-schedule float64 steps of the same workload "
+                       f"(l={l}, numpy, 1 thread): {t_used:.1f} s",
+                ms_per_step=1e3 * t_used / steps)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--batch-size", type=int, default=100)
+    ap.add_argument("--graph-chunk", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-iters", type=int, default=200)
+    args = ap.parse_args()
+
+    import torch
+    from rae import dist as rdist
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+
+    ws, rk, lrank = rdist.init()
+    if ws != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    dev = torch.device("cuda", lrank)
+    torch.cuda.set_device(dev)
+    cfg = CONFIGS[args.config]
+    l = args.batch_size
+    L = l * ws
+    t0 = time.perf_counter()
+    data, gold = synthetic_dataset(cfg["N"], cfg["d"], cfg["ntrue"], seed=1234)
+    t_data = time.perf_counter() - t0
+    exchange = rdist.make_exchange(ws, rk)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, cfg["r"], cfg["m"],
+                             cfg["s"], 0.0, 0.0, "adagrad", "bench", cfg["dec"], False, True, False,
+                             1.0, device=dev, world_size=ws, rank=rk, exchange=exchange,
+                             graph_chunk=args.graph_chunk)
+    ind.compile_function()
+    eng = ind.engine
+    t0 = time.perf_counter()
+    neg1, neg2 = ind.draw_epoch_negatives()
+    t_neg = time.perf_counter() - t0
+    eng.set_epoch_negatives(neg1, neg2)
+    rdist.warm_up(exchange, eng.exchange_buf)
+    nb = eng.nb
+    K, W = args.steps, args.warmup
+    if K + W > nb:
+        raise SystemExit(f"steps+warmup={K + W} exceed the {nb} global batches of one epoch")
+
+    eng.run(0, W)                          # includes graph capture
+    torch.cuda.synchronize()
+    rdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run(W, K)
+    torch.cuda.synchronize()
+    rdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = rdist.max_over_ranks(time.perf_counter() - t0)
+    eng.check()
+    costs = eng.costs[W:W + K].cpu().numpy()
+    assert np.all(np.isfinite(costs)), "non-finite cost"
+
+    # ---- per-kernel durations with HIP events on the launch stream (eager launches of
+    # the same step sequence continuing the epoch)
+    lib, plan = eng.lib, eng.plan
+    st = torch.cuda.current_stream()
+    sp_ = C.c_void_p(st.cuda_stream)
+    b0 = W + K
+    n_it = min(args.kernel_iters, nb - b0)
+    lib.rae_set_cursor(plan, b0, sp_)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+            torch.cuda.Event(enable_timing=True)) for _ in range(n_it)]
+    for i, (e0, e1, e2) in enumerate(evs):
+        e0.record(st)
+        lib.rae_step_forward(plan, i, sp_)
+        e1.record(st)
+        if exchange is not None:
+            exchange(eng.exchange_buf)
+        lib.rae_step_update(plan, i, sp_)
+        e2.record(st)
+    torch.cuda.synchronize()
+    fwd_ms = np.array([a.elapsed_time(b) for a, b, _ in evs])
+    upd_ms = np.array([b.elapsed_time(c) for _, b, c in evs])
+    fwd_us = float(np.mean(fwd_ms) * 1e3)
+    upd_us = float(np.mean(upd_ms) * 1e3)
+    indptr = eng.split.indptr_np
+    fb = np.mean([forward_bytes(indptr, (b0 + i) * L, L, cfg["m"], cfg["r"], cfg["s"],
+                                eng.rec_floats, cfg["dec"]) for i in range(n_it)])
+    achieved = fb / (fwd_us * 1e-6) / 1e9
+
+    ms_per_step = 1e3 * elapsed / K
+    out = {
+        "metric": METRIC,
+        "value": K * L / elapsed,
+        "unit": "examples/s",
+        "n_gpus": ws,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (SURVEY 8d generator, seed 1234; random-init params, seed 2)",
+        "config": {"workload": cfg["name"], "global_batch": L, "batch_per_gpu": l,
+                   "n_examples": cfg["N"], "n_features": cfg["d"], "relations": cfg["m"],
+                   "embed": cfg["r"], "neg_samples": cfg["s"], "decoder": cfg["dec"],
+                   "optimizer": "adagrad", "parallelism": f"dp{ws}",
+                   "n_entities": data.get_arg_voc_size(), "graph_chunk": args.graph_chunk},
+        "roofline": {"kernel": "k_forward (index WGs + per-example encoder/decoder fwd+bwd)",
+                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "bytes_per_launch": fb, "avg_launch_us": fwd_us,
+                     "timing": "HIP events around eager launches on the launch stream"},
+        "kernel_us": {"forward": fwd_us, "update": upd_us,
+                      "forward_p50": float(np.median(fwd_ms) * 1e3),
+                      "update_p50": float(np.median(upd_ms) * 1e3)},
+        "negative_sampling_s": t_neg,
+        "dataset_build_s": t_data,
+    }
+    if rk == 0 and ws == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(data, cfg, l, args.cpu_seconds)
+        out["cpu_baseline"]["host_cpus"] = os.cpu_count()
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    if rk == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -32,16 +32,16 @@ using namespace rae;
 // kernels
 // ======================================================================================
 template <int DEC, bool V4>
-__global__ __launch_bounds__(RAE_BT) void k_forward(StepArgs a) {
+__global__ __launch_bounds__(RAE_FBT) void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = *a.cursor + a.step_offset;
     const int bid = blockIdx.x;
     if (bid < a.HA) {
-        build_index_partition(a, g, true, bid, smem);
+        build_index_partition<RAE_FBT>(a, g, true, bid, smem);
         return;
     }
     if (bid < a.HA + a.HW) {
-        build_index_partition(a, g, false, bid - a.HA, smem);
+        build_index_partition<RAE_FBT>(a, g, false, bid - a.HA, smem);
         return;
     }
     const int bl = bid - a.HA - a.HW;
@@ -49,44 +49,61 @@ __global__ __launch_bounds__(RAE_BT) void k_forward(StepArgs a) {
     else bilinear_example<V4>(a, g, bl, smem, DEC == RAE_DEC_HYBRID);
 }
 
-template <int OPT, bool V4>
+__host__ __device__ inline int n_ctiles(int dec, int r, int m) {
+    return dec != RAE_DEC_RESCAL ? 2 * ((r + 15) / 16) * ((m + 15) / 16) : 0;
+}
+__host__ __device__ inline int n_rtiles(int dec, int r, int m) {
+    return dec != RAE_DEC_SP ? ((r * r + 15) / 16) * ((m + 15) / 16) : 0;
+}
+
+template <int OPT, bool V4, int Q, bool BIL>
 __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
     const int nw = gridDim.x * RAE_NWAVE;
     const int64_t g = *a.cursor + a.step_offset;
     const int64_t ex0 = g * (int64_t)a.L;
+    const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
+    const int nCt = n_ctiles(a.dec, a.r, a.m);
+    const int nRt = n_rtiles(a.dec, a.r, a.m);
     const int TA = total_rows(a.hdrA, a.HA);
     const int TW = total_rows(a.hdrW, a.HW);
-    const int nC = (a.dec != RAE_DEC_RESCAL) ? 2 * a.r : 0;
-    const int nR = (a.dec != RAE_DEC_SP) ? a.r * a.r : 0;
-    const int T = nC + TA + TW + nR + 1;
+    const int T = nCt + nRt + mt + 1 + TA + TW;
     for (int t = gw; t < T; t += nw) {
         int tt = t;
-        if (tt < nC) {
-            task_sp_matrix_row<OPT>(a, tt / a.r, tt % a.r, tt, lane);
+        if (tt < nCt) {
+            const int which = tt / (rt * mt), ti = tt - which * rt * mt;
+            task_mfma_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
+                                which ? a.lay.odw2 : a.lay.odw1, false, (ti / mt) * 16,
+                                (ti % mt) * 16, t, lane);
             continue;
         }
-        tt -= nC;
+        tt -= nCt;
+        if (BIL && tt < nRt) {
+            task_bilinear_tile<OPT>(a, (tt / mt) * 16, (tt % mt) * 16, nCt + tt, lane);
+            continue;
+        }
+        tt -= nRt;
+        if (tt < mt) {
+            task_mfma_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, tt * 16, 0, lane);
+            continue;
+        }
+        tt -= mt;
+        if (tt == 0) {
+            task_cost(a, lane);
+            continue;
+        }
+        tt -= 1;
         if (tt < TA) {
             int u;
             const int h = locate_row(a.hdrA, a.HA, tt, &u);
-            task_entity_row<OPT, V4>(a, h, u, lane);
+            task_entity_row<OPT, V4, Q, BIL>(a, h, u, lane);
             continue;
         }
         tt -= TA;
-        if (tt < TW) {
-            int u;
-            const int h = locate_row(a.hdrW, a.HW, tt, &u);
-            task_feature_row<OPT, V4>(a, ex0, h, u, lane);
-            continue;
-        }
-        tt -= TW;
-        if (tt < nR) {
-            task_bilinear_row<OPT>(a, tt, nC + tt, lane);
-            continue;
-        }
-        task_bias_and_cost<OPT>(a, ex0, lane);
+        int u;
+        const int h = locate_row(a.hdrW, a.HW, tt, &u);
+        task_feature_row<OPT, V4, Q>(a, ex0, h, u, lane);
     }
 }
 
@@ -236,6 +253,7 @@ struct rae_plan {
     size_t smem_fwd = 0;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
+    int q = 1;
 };
 
 extern "C" const char* rae_last_error(void) { return g_last_error.c_str(); }
@@ -323,12 +341,23 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples);
     a.costs = buf->costs;
     p->v4 = (c.relations % 4 == 0) && (c.embed % 4 == 0);
+    {
+        const int vw = p->v4 ? 4 : 1;
+        const int qa = ceil_div(c.embed / vw, 64), qm = ceil_div(c.relations / vw, 64);
+        const int q = qa > qm ? qa : qm;
+        if (q > 2) {
+            delete p;
+            return fail(RAE_E_INVALID,
+                        "relations/embed are limited to 512 (128 when not multiples of 4)");
+        }
+        p->q = q <= 1 ? 1 : 2;
+    }
 
     // row-index partitions: ~1024 records per partition on average, LDS holds RAE_KCAP
     a.RA = L * NJ;
     a.RW = c.max_batch_nnz > 0 ? c.max_batch_nnz : 1;
-    a.HA = ceil_div(a.RA, 1024);
-    a.HW = ceil_div(a.RW, 1024);
+    a.HA = ceil_div(a.RA, RAE_PART);
+    a.HW = ceil_div(a.RW, RAE_PART);
     int bbits = 1;
     while ((1 << bbits) < L) ++bbits;
     a.posbits = 31 - bbits;
@@ -337,8 +366,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "an example has too many features for the record encoding");
     }
     // parameter / dense-row partial slots for the regulariser
-    a.nregC = (c.decoder != RAE_DEC_RESCAL ? 2 * c.embed : 0) +
-              (c.decoder != RAE_DEC_SP ? c.embed * c.embed : 0);
+    a.nregC = n_ctiles(c.decoder, c.embed, c.relations) + n_rtiles(c.decoder, c.embed, c.relations);
     p->grid_dense = 1024;
     a.nregW = a.reg_on ? p->grid_dense : 0;
 
@@ -382,7 +410,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    const size_t smem_idx = 8ull * RAE_KCAP + 4ull * 16;
+    const size_t smem_idx = 8ull * RAE_KCAP + 4ull * (33 + L + 1);
     p->smem_fwd = smem_ex > smem_idx ? smem_ex : smem_idx;
     if (p->smem_fwd > 160 * 1024) {
         (void)hipFree(p->ws);
@@ -390,9 +418,20 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
     }
     p->grid_fwd = a.HA + a.HW + c.batch_size;
-    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + 1;
+    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + (c.relations + 15) / 16 + 1;
     int gu = ceil_div(tasks, RAE_NWAVE);
-    p->grid_update = gu < 1 ? 1 : (gu > 4096 ? 4096 : gu);
+    p->grid_update = gu < 1 ? 1 : (gu > 8192 ? 8192 : gu);
+    {
+        const void* fns[] = {(const void*)k_forward<RAE_DEC_SP, true>,
+                             (const void*)k_forward<RAE_DEC_SP, false>,
+                             (const void*)k_forward<RAE_DEC_RESCAL, true>,
+                             (const void*)k_forward<RAE_DEC_RESCAL, false>,
+                             (const void*)k_forward<RAE_DEC_HYBRID, true>,
+                             (const void*)k_forward<RAE_DEC_HYBRID, false>};
+        for (const void* f : fns)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)p->smem_fwd);
+    }
     *out = p;
     return RAE_OK;
 }
@@ -432,9 +471,9 @@ extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t strea
 template <int DEC>
 static void launch_fwd_dec(rae_plan* p, const StepArgs& a, hipStream_t st) {
     if (p->v4)
-        hipLaunchKernelGGL((k_forward<DEC, true>), dim3(p->grid_fwd), dim3(RAE_BT), p->smem_fwd, st, a);
+        hipLaunchKernelGGL((k_forward<DEC, true>), dim3(p->grid_fwd), dim3(RAE_FBT), p->smem_fwd, st, a);
     else
-        hipLaunchKernelGGL((k_forward<DEC, false>), dim3(p->grid_fwd), dim3(RAE_BT), p->smem_fwd, st, a);
+        hipLaunchKernelGGL((k_forward<DEC, false>), dim3(p->grid_fwd), dim3(RAE_FBT), p->smem_fwd, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
@@ -451,18 +490,29 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     return RAE_OK;
 }
 
+template <int OPT, bool V4, bool BIL>
+static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
+    if (p->q == 1) hipLaunchKernelGGL((k_update<OPT, V4, 1, BIL>), gu, bt, 0, st, a);
+    else hipLaunchKernelGGL((k_update<OPT, V4, 2, BIL>), gu, bt, 0, st, a);
+}
+template <int OPT, bool V4>
+static void launch_update_v(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
+    if (a.dec == RAE_DEC_SP) launch_update_b<OPT, V4, false>(p, gu, bt, st, a);
+    else launch_update_b<OPT, V4, true>(p, gu, bt, st, a);
+}
+template <int OPT>
+static void launch_update_q(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
+    if (p->v4) launch_update_v<OPT, true>(p, gu, bt, st, a);
+    else launch_update_v<OPT, false>(p, gu, bt, st, a);
+}
+
 static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
     StepArgs a = p->args;
     a.cursor = cursor;
     a.step_offset = off;
     const dim3 gu(p->grid_update), bt(RAE_BT);
-    if (a.opt == RAE_OPT_ADAGRAD) {
-        if (p->v4) hipLaunchKernelGGL((k_update<0, true>), gu, bt, 0, st, a);
-        else hipLaunchKernelGGL((k_update<0, false>), gu, bt, 0, st, a);
-    } else {
-        if (p->v4) hipLaunchKernelGGL((k_update<1, true>), gu, bt, 0, st, a);
-        else hipLaunchKernelGGL((k_update<1, false>), gu, bt, 0, st, a);
-    }
+    if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
+    else launch_update_q<1>(p, gu, bt, st, a);
     HIPCHK(hipGetLastError());
     if (a.reg_on) {
         if (a.opt == RAE_OPT_ADAGRAD)

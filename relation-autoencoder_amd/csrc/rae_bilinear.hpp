@@ -12,7 +12,7 @@ __device__ void bilinear_example(const StepArgs& a, int64_t g, int bl, char* sme
 }
 
 template <int OPT>
-__device__ void task_bilinear_row(const StepArgs& a, int t, int slot, int lane) {
+__device__ void task_bilinear_tile(const StepArgs& a, int i0, int k0, int slot, int lane) {
     __builtin_trap();
 }
 

@@ -11,17 +11,19 @@
 // FIXED order (row, record id) -- the per-row gradient sums are then deterministic and
 // identical on every data-parallel rank.
 //
-// Records are hash-partitioned by row % H; partition h is built by one workgroup:
-//   gather its records -> 64-bit keys (row << 32 | rec) in LDS -> bitonic sort ->
-//   head flags + block scan -> unique rows with segment starts.
+// Records are hash-partitioned by row % H (~RAE_PART records per partition); partition h
+// is built by one workgroup: load its records' rows with coalesced, independent loads ->
+// 64-bit keys (row << 32 | rec) -> bitonic sort (in registers + wave shuffles for strides
+// < 64, through LDS for larger strides) -> head flags + block scan -> unique rows.
 #pragma once
 #include "rae_common.hpp"
 #include "rae_step.hpp"
 
 namespace rae {
 
-// Block-wide exclusive scan of a 0/1 flag (RAE_BT threads). Returns this thread's
-// exclusive prefix; *total receives the block total.  `ws` is >= RAE_NWAVE+1 ints.
+// Block-wide exclusive scan of a 0/1 flag (BT threads).  Returns this thread's exclusive
+// prefix; *total receives the block total.  `ws` is >= BT/64 ints.
+template <int BT>
 __device__ __forceinline__ int block_flag_scan(int flag, int* ws, int* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long bal = __ballot(flag);
@@ -32,7 +34,7 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* ws, int* total) {
     __syncthreads();
     int off = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < RAE_NWAVE; ++i) {
+    for (int i = 0; i < BT / 64; ++i) {
         const int c = ws[i];
         off += (i < w) ? c : 0;
         tot += c;
@@ -41,14 +43,71 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* ws, int* total) {
     return off + pre;
 }
 
+// bitonic compare-exchange step for the element held by thread `i`
+__device__ __forceinline__ unsigned long long bitonic_pick(unsigned long long mine,
+                                                           unsigned long long other, int i,
+                                                           int j, int k) {
+    const bool up = (i & k) == 0;
+    const bool lower = (i & j) == 0;
+    const unsigned long long lo = mine < other ? mine : other;
+    const unsigned long long hi = mine < other ? other : mine;
+    return (lower == up) ? lo : hi;
+}
+
+template <int BT>
+__device__ void sort_keys(unsigned long long* keys, int n2) {
+    const int tid = threadIdx.x;
+    if (n2 <= BT) {
+        // one key per thread: strides < 64 through wave shuffles, larger through LDS
+        unsigned long long key = keys[tid];
+        for (int k = 2; k <= n2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                unsigned long long other;
+                if (j >= 64) {
+                    __syncthreads();
+                    keys[tid] = key;
+                    __syncthreads();
+                    other = keys[tid ^ j];
+                } else {
+                    other = shfl_xor_u64(key, j);
+                }
+                key = bitonic_pick(key, other, tid, j, k);
+            }
+        }
+        __syncthreads();
+        keys[tid] = key;
+        __syncthreads();
+        return;
+    }
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < n2; i += BT) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = keys[i], y = keys[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        keys[i] = y;
+                        keys[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // isA: entity-row index (A / Ab), records (b, j), j < 2+2s:
 //   j = 0 -> e1, 1 -> e2, 2+t -> neg1[t], 2+s+t -> neg2[t]        (rec = b*NJ + j)
 // !isA: feature-row index (W), records = CSR entries of the batch:
 //   rec = b << posbits | position-in-row
+template <int BT>
 __device__ void build_index_partition(const StepArgs& a, int64_t g, bool isA, int h,
                                       char* smem) {
+    constexpr int E = 16;                      // records per thread per pass
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);   // [0] count, [1..] scan scratch
+    int* sptr = sint + 32;                                   // batch indptr (W index)
     const int tid = threadIdx.x;
     const int H = isA ? a.HA : a.HW;
     const int R = isA ? a.RA : a.RW;
@@ -58,38 +117,66 @@ __device__ void build_index_partition(const StepArgs& a, int64_t g, bool isA, in
     int32_t* ustart = (isA ? a.ustartA : a.ustartW) + (int64_t)h * R;
 
     if (tid == 0) sint[0] = 0;
-    __syncthreads();
     const int64_t ex0 = g * (int64_t)a.L;
+    if (!isA)
+        for (int b = tid; b <= a.L; b += BT) sptr[b] = a.indptr[ex0 + b];
+    __syncthreads();
     if (isA) {
         const int NJ = 2 + 2 * a.s;
         const int nrec = a.L * NJ;
-        for (int rec = tid; rec < nrec; rec += RAE_BT) {
-            const int b = rec / NJ;
-            const int j = rec - b * NJ;
-            const int64_t ex = ex0 + b;
-            const int64_t col = a.neg_mode ? ex : (int64_t)b;
-            int row;
-            if (j == 0) row = a.args1[ex];
-            else if (j == 1) row = a.args2[ex];
-            else if (j < 2 + a.s) row = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
-            else row = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
-            if (row % H == h) {
-                const int slot = atomicAdd(&sint[0], 1);
-                if (slot < RAE_KCAP)
-                    keys[slot] = ((unsigned long long)(unsigned)row << 32) | (unsigned)rec;
+        // enumerate j-major (consecutive threads -> consecutive columns: coalesced)
+        for (int base = 0; base < nrec; base += BT * E) {
+            int rows[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int idx = base + tid + BT * e;
+                rows[e] = -1;
+                if (idx < nrec) {
+                    const int j = idx / a.L, b = idx - j * a.L;
+                    const int64_t ex = ex0 + b;
+                    const int64_t col = a.neg_mode ? ex : (int64_t)b;
+                    if (j == 0) rows[e] = a.args1[ex];
+                    else if (j == 1) rows[e] = a.args2[ex];
+                    else if (j < 2 + a.s) rows[e] = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
+                    else rows[e] = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int idx = base + tid + BT * e;
+                if (rows[e] >= 0 && rows[e] % H == h) {
+                    const int j = idx / a.L, b = idx - j * a.L;
+                    const unsigned rec = (unsigned)(b * NJ + j);
+                    const int slot = atomicAdd(&sint[0], 1);
+                    if (slot < RAE_KCAP)
+                        keys[slot] = ((unsigned long long)(unsigned)rows[e] << 32) | rec;
+                }
             }
         }
     } else {
-        for (int b = tid; b < a.L; b += RAE_BT) {
-            const int64_t ex = ex0 + b;
-            const int p0 = a.indptr[ex], p1 = a.indptr[ex + 1];
-            for (int p = p0; p < p1; ++p) {
-                const int row = a.indices[p];
-                if (row % H == h) {
+        const int P0 = sptr[0], nnz = sptr[a.L] - P0;
+        for (int base = 0; base < nnz; base += BT * E) {
+            int rows[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int idx = base + tid + BT * e;
+                rows[e] = (idx < nnz) ? a.indices[P0 + idx] : -1;
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int idx = base + tid + BT * e;
+                if (rows[e] >= 0 && rows[e] % H == h) {
+                    // example of nnz position P0+idx: binary search in the batch indptr
+                    int lo = 0, hi = a.L - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (sptr[mid] - P0 <= idx) lo = mid; else hi = mid - 1;
+                    }
+                    const unsigned rec =
+                        ((unsigned)lo << a.posbits) | (unsigned)(idx - (sptr[lo] - P0));
                     const int slot = atomicAdd(&sint[0], 1);
-                    const unsigned rec = ((unsigned)b << a.posbits) | (unsigned)(p - p0);
                     if (slot < RAE_KCAP)
-                        keys[slot] = ((unsigned long long)(unsigned)row << 32) | rec;
+                        keys[slot] = ((unsigned long long)(unsigned)rows[e] << 32) | rec;
                 }
             }
         }
@@ -106,28 +193,13 @@ __device__ void build_index_partition(const StepArgs& a, int64_t g, bool isA, in
     }
     int n2 = 1;
     while (n2 < cnt) n2 <<= 1;
-    for (int i = cnt + tid; i < n2; i += RAE_BT) keys[i] = ~0ull;
+    const int npad = n2 > BT ? n2 : BT;
+    for (int i = cnt + tid; i < npad; i += BT) keys[i] = ~0ull;
     __syncthreads();
-    // bitonic sort, ascending
-    for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < n2; i += RAE_BT) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = keys[i], y = keys[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        keys[i] = y;
-                        keys[ixj] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
+    sort_keys<BT>(keys, n2);
     // segmentation
     int base = 0;
-    for (int i0 = 0; i0 < cnt; i0 += RAE_BT) {
+    for (int i0 = 0; i0 < cnt; i0 += BT) {
         const int i = i0 + tid;
         int head = 0;
         unsigned row = 0;
@@ -138,7 +210,7 @@ __device__ void build_index_partition(const StepArgs& a, int64_t g, bool isA, in
             srec[i] = (int32_t)(unsigned)(k & 0xffffffffull);
         }
         int tot;
-        const int u = base + block_flag_scan(head, sint + 1, &tot);
+        const int u = base + block_flag_scan<BT>(head, sint + 1, &tot);
         if (head) {
             urow[u] = (int32_t)row;
             ustart[u] = i;

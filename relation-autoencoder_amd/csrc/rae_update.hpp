@@ -8,6 +8,10 @@
 // skipping them is exact.  With lambda1/lambda2 != 0 every W element has a non-zero
 // regulariser gradient: then the W rows are only reduced into a dense scratch here and the
 // dense sweep kernel (k_dense_w) applies the full update, as the reference does.
+//
+// Work items of k_update, one wavefront each (grid-strided):
+//   dense decoder-matrix tiles (16x16, MFMA), Wb tiles, the batch cost,
+//   one wave per referenced A row, one wave per referenced W row.
 #pragma once
 #include "rae_common.hpp"
 #include "rae_index.hpp"
@@ -15,254 +19,279 @@
 
 namespace rae {
 
-#define RAE_MAXQ 4   // float4 chunks per lane: rows up to 4*64*4 = 1024 floats
 
-// update one contiguous parameter row held as float4 chunks g[] (lane-strided)
-template <int OPT>
-__device__ __forceinline__ void update_row4(float* p, float* acc, const float4* g, int nq,
-                                            float lr, int lane) {
-    float4* p4 = reinterpret_cast<float4*>(p);
-    float4* a4 = reinterpret_cast<float4*>(acc);
-#pragma unroll
-    for (int cc = 0; cc < RAE_MAXQ; ++cc) {
-        const int c = lane + RAE_WAVE * cc;
-        if (c < nq) {
-            float4 v = p4[c];
-            float4 ac = (OPT == 0) ? a4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-            v.x = opt_update<OPT>(v.x, &ac.x, g[cc].x, lr);
-            v.y = opt_update<OPT>(v.y, &ac.y, g[cc].y, lr);
-            v.z = opt_update<OPT>(v.z, &ac.z, g[cc].z, lr);
-            v.w = opt_update<OPT>(v.w, &ac.w, g[cc].w, lr);
-            p4[c] = v;
-            if (OPT == 0) a4[c] = ac;
-        }
-    }
-}
+// ---- dense decoder-matrix tiles on MFMA ---------------------------------------------
+// Gradient of a 16x16 tile of a matrix M (nrows x m) whose gradient is
+//   G[i][k] = sum_b coef(b, i) * P_b[k]      (a batch-contracted outer-product sum)
+// computed with v_mfma_f32_16x16x4_f32 (exact fp32, k-ordered fma chain -> deterministic):
+//   A[i][b] = coef(b, i)   lane l holds A[l&15][b0 + (l>>4)]
+//   B[b][k] = P_b[k]       lane l holds B[b0 + (l>>4)][l&15]
+//   D[row][col]            col = lane&15, row = (lane>>4)*4 + reg
+// SP/hybrid C1, C2: coef(b, i) = dw1_b[i] / dw2_b[i]; Wb (ones): one row of ones times dS_b.
+typedef float rae_f4 __attribute__((ext_vector_type(4)));
+#define RAE_TU 8     // k-steps (x4 examples) whose operands are loaded before the MFMA chain
 
 template <int OPT>
-__device__ __forceinline__ void update_row1(float* p, float* acc, const float* g, int n,
-                                            float lr, int lane) {
+__device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw,
+                               bool ones, int i0, int k0, int slot, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    const int m = a.m, L = a.L;
+    const int i = i0 + li, k = k0 + li;
+    const bool iv = i < nrows, kv = k < m;
+    const int ic = iv ? i : 0, kc = kv ? k : 0;
+    rae_f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int b0 = 0; b0 < L; b0 += 4 * RAE_TU) {
+        float av[RAE_TU], bv[RAE_TU];
 #pragma unroll
-    for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-        const int c = lane + RAE_WAVE * cc;
-        if (c < n) {
-            float ac = (OPT == 0) ? acc[c] : 0.f;
-            p[c] = opt_update<OPT>(p[c], &ac, g[cc], lr);
-            if (OPT == 0) acc[c] = ac;
+        for (int u = 0; u < RAE_TU; ++u) {
+            const int b = b0 + 4 * u + lk;
+            const bool bvld = b < L;
+            const float* er = a.ex + (int64_t)(bvld ? b : 0) * a.lay.rec;
+            const float x = ones ? 1.f : er[odw + ic];
+            const float y = er[(ones ? a.lay.odS : a.lay.oP) + kc];   // Wb: sum_b dS_b
+            av[u] = (bvld && iv && (!ones || li == 0)) ? x : 0.f;
+            bv[u] = (bvld && kv) ? y : 0.f;
         }
+#pragma unroll
+        for (int u = 0; u < RAE_TU; ++u)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
     }
-}
-
-__device__ __forceinline__ void fma4(float4& g, float s, const float4 v) {
-    g.x += s * v.x; g.y += s * v.y; g.z += s * v.z; g.w += s * v.w;
-}
-
-// ---- A / Ab rows ---------------------------------------------------------------------
-template <int OPT, bool V4>
-__device__ void task_entity_row(const StepArgs& a, int h, int u, int lane) {
-    const int r = a.r, NJ = 2 + 2 * a.s;
-    const int32_t* hdr = a.hdrA + 2 * h;
-    const int64_t base = (int64_t)h * a.RA;
-    const int e = a.urowA[base + u];
-    const int st = a.ustartA[base + u];
-    const int en = (u + 1 < hdr[1]) ? a.ustartA[base + u + 1] : hdr[0];
-    const bool xy = a.dec != 0;
-    float gb = 0.f;
-    if (V4) {
-        const int nq = r >> 2;
-        float4 g[RAE_MAXQ];
+    const int col = k0 + li;
+    float l1 = 0.f, l2 = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < RAE_MAXQ; ++cc) g[cc] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int i = st; i < en; ++i) {
-            const int rec = a.srecA[base + i];
-            const int b = rec / NJ, j = rec - b * NJ;
-            const float* er = a.ex + (int64_t)b * a.lay.rec;
-            const float al = er[a.lay.ocoef + 3 * j];
-            const float be = er[a.lay.ocoef + 3 * j + 1];
-            gb += er[a.lay.ocoef + 3 * j + 2];
-            const float4* V1 = reinterpret_cast<const float4*>(er + a.lay.oV1);
-            const float4* V2 = reinterpret_cast<const float4*>(er + a.lay.oV2);
-#pragma unroll
-            for (int cc = 0; cc < RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < nq) {
-                    if (al != 0.f) fma4(g[cc], al, V1[c]);
-                    if (be != 0.f) fma4(g[cc], be, V2[c]);
-                    if (xy && j < 2) {
-                        const float4* XY =
-                            reinterpret_cast<const float4*>(er + (j == 0 ? a.lay.oX : a.lay.oY));
-                        fma4(g[cc], 1.f, XY[c]);
-                    }
-                }
-            }
-        }
-        update_row4<OPT>(a.A + (int64_t)e * r, a.aA ? a.aA + (int64_t)e * r : nullptr, g, nq,
-                         a.lr, lane);
-    } else {
-        float g[4 * RAE_MAXQ];
-#pragma unroll
-        for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) g[cc] = 0.f;
-        for (int i = st; i < en; ++i) {
-            const int rec = a.srecA[base + i];
-            const int b = rec / NJ, j = rec - b * NJ;
-            const float* er = a.ex + (int64_t)b * a.lay.rec;
-            const float al = er[a.lay.ocoef + 3 * j];
-            const float be = er[a.lay.ocoef + 3 * j + 1];
-            gb += er[a.lay.ocoef + 3 * j + 2];
-#pragma unroll
-            for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < r) {
-                    if (al != 0.f) g[cc] += al * er[a.lay.oV1 + c];
-                    if (be != 0.f) g[cc] += be * er[a.lay.oV2 + c];
-                    if (xy && j < 2) g[cc] += er[(j == 0 ? a.lay.oX : a.lay.oY) + c];
-                }
-            }
-        }
-        update_row1<OPT>(a.A + (int64_t)e * r, a.aA ? a.aA + (int64_t)e * r : nullptr, g, r,
-                         a.lr, lane);
-    }
-    if (lane == 0) {
-        float ac = (OPT == 0) ? a.aAb[e] : 0.f;
-        a.Ab[e] = opt_update<OPT>(a.Ab[e], &ac, gb, a.lr);
-        if (OPT == 0) a.aAb[e] = ac;
-    }
-}
-
-// ---- W rows ---------------------------------------------------------------------------
-template <int OPT, bool V4>
-__device__ void task_feature_row(const StepArgs& a, int64_t g0, int h, int u, int lane) {
-    const int m = a.m;
-    const int32_t* hdr = a.hdrW + 2 * h;
-    const int64_t base = (int64_t)h * a.RW;
-    const int f = a.urowW[base + u];
-    const int st = a.ustartW[base + u];
-    const int en = (u + 1 < hdr[1]) ? a.ustartW[base + u + 1] : hdr[0];
-    const unsigned mask = (1u << a.posbits) - 1u;
-    if (V4) {
-        const int nq = m >> 2;
-        float4 g[RAE_MAXQ];
-#pragma unroll
-        for (int cc = 0; cc < RAE_MAXQ; ++cc) g[cc] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int i = st; i < en; ++i) {
-            const unsigned rec = (unsigned)a.srecW[base + i];
-            const int b = (int)(rec >> a.posbits);
-            float val = 1.f;
-            if (a.values) val = a.values[a.indptr[g0 + b] + (int)(rec & mask)];
-            const float4* dS =
-                reinterpret_cast<const float4*>(a.ex + (int64_t)b * a.lay.rec + a.lay.odS);
-#pragma unroll
-            for (int cc = 0; cc < RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < nq) fma4(g[cc], val, dS[c]);
-            }
-        }
-        if (a.reg_on) {
-            float4* gs = reinterpret_cast<float4*>(a.gWs + (int64_t)f * m);
-#pragma unroll
-            for (int cc = 0; cc < RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < nq) gs[c] = g[cc];
-            }
-        } else {
-            update_row4<OPT>(a.W + (int64_t)f * m, a.aW ? a.aW + (int64_t)f * m : nullptr, g, nq,
-                             a.lr, lane);
-        }
-    } else {
-        float g[4 * RAE_MAXQ];
-#pragma unroll
-        for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) g[cc] = 0.f;
-        for (int i = st; i < en; ++i) {
-            const unsigned rec = (unsigned)a.srecW[base + i];
-            const int b = (int)(rec >> a.posbits);
-            float val = 1.f;
-            if (a.values) val = a.values[a.indptr[g0 + b] + (int)(rec & mask)];
-            const float* dS = a.ex + (int64_t)b * a.lay.rec + a.lay.odS;
-#pragma unroll
-            for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < m) g[cc] += val * dS[c];
-            }
-        }
-        if (a.reg_on) {
-#pragma unroll
-            for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-                const int c = lane + RAE_WAVE * cc;
-                if (c < m) a.gWs[(int64_t)f * m + c] = g[cc];
-            }
-        } else {
-            update_row1<OPT>(a.W + (int64_t)f * m, a.aW ? a.aW + (int64_t)f * m : nullptr, g, m,
-                             a.lr, lane);
-        }
-    }
-}
-
-// ---- dense decoder rows (C1 / C2 rows of m): gC[i,:] = sum_b dw[b,i] P[b,:] -------------
-template <int OPT>
-__device__ void task_sp_matrix_row(const StepArgs& a, int which, int i, int slot, int lane) {
-    const int m = a.m;
-    float* C = which ? a.C2 : a.C1;
-    float* aC = which ? a.aC2 : a.aC1;
-    const int odw = which ? a.lay.odw2 : a.lay.odw1;
-    float g[4 * RAE_MAXQ];
-#pragma unroll
-    for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) g[cc] = 0.f;
-    for (int b = 0; b < a.L; ++b) {
-        const float* er = a.ex + (int64_t)b * a.lay.rec;
-        const float dw = er[odw + i];
-#pragma unroll
-        for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-            const int k = lane + RAE_WAVE * cc;
-            if (k < m) g[cc] += dw * er[a.lay.oP + k];
-        }
-    }
-    float* row = C + (int64_t)i * m;
-    if (a.reg_on && a.ext_reg) {
-        float l1 = 0.f, l2 = 0.f;
-#pragma unroll
-        for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-            const int k = lane + RAE_WAVE * cc;
-            if (k < m) {
-                const float w = row[k];
-                g[cc] += a.l1adj * sgnf(w) + 2.f * a.l2adj * w;
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = i0 + lk * 4 + reg;
+        if (row < nrows && col < m && (!ones || row == i0)) {
+            const int64_t o = ones ? col : (int64_t)row * m + col;
+            const float w = M[o];
+            float g = acc[reg];
+            if (!ones && a.reg_on && a.ext_reg) {
+                g += a.l1adj * sgnf(w) + 2.f * a.l2adj * w;
                 l1 += fabsf(w);
                 l2 += w * w;
             }
+            float ac = (OPT == 0) ? aM[o] : 0.f;
+            M[o] = opt_update<OPT>(w, &ac, g, a.lr);
+            if (OPT == 0) aM[o] = ac;
         }
+    }
+    if (!ones && a.reg_on && a.ext_reg) {
         const double L1 = wave_sum_d((double)l1), L2 = wave_sum_d((double)l2);
         if (lane == 0) {
             a.regpart[2 * slot] = L1;
             a.regpart[2 * slot + 1] = L2;
         }
     }
-    update_row1<OPT>(row, aC ? aC + (int64_t)i * m : nullptr, g, m, a.lr, lane);
 }
 
-// ---- Wb + the batch cost --------------------------------------------------------------
-template <int OPT>
-__device__ void task_bias_and_cost(const StepArgs& a, int64_t g0, int lane) {
-    const int m = a.m;
-    float g[4 * RAE_MAXQ];
-#pragma unroll
-    for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) g[cc] = 0.f;
+// ---- the batch cost: -mean(all_scores) = -(sum_b loss_b) / (4L + 2Ls)  (OieModel.py:90)
+__device__ void task_cost(const StepArgs& a, int lane) {
     double loss = 0.0;
-    for (int b = 0; b < a.L; ++b) {
-        const float* er = a.ex + (int64_t)b * a.lay.rec;
-#pragma unroll
-        for (int cc = 0; cc < 4 * RAE_MAXQ; ++cc) {
-            const int k = lane + RAE_WAVE * cc;
-            if (k < m) g[cc] += er[a.lay.odS + k];
-        }
-    }
-    for (int b = lane; b < a.L; b += RAE_WAVE) loss += (double)a.ex[(int64_t)b * a.lay.rec + a.lay.oloss];
+    for (int b = lane; b < a.L; b += RAE_WAVE)
+        loss += (double)a.ex[(int64_t)b * a.lay.rec + a.lay.oloss];
     loss = wave_sum_d(loss);
-    update_row1<OPT>(a.Wb, a.aWb, g, m, a.lr, lane);
     if (lane == 0) {
         const double D = 4.0 * a.L + 2.0 * a.L * a.s;
-        const float cost = (float)(-loss / D);        // -mean(all_scores), OieModel.py:90
+        const float cost = (float)(-loss / D);
         const int64_t batch = *a.cursor + a.step_offset;
         if (a.reg_on) *a.base_cost = cost;
         else a.costs[batch] = cost;
+    }
+}
+
+// ---- one parameter row held as lane-strided vectors (Q per lane) ----------------------
+template <bool V4, int Q>
+struct RowVec {
+    typedef typename VecT<V4>::T VT;
+    VT v[Q];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) vzero(v[q]);
+    }
+    __device__ __forceinline__ void load(const float* p, int nv, int lane) {
+        const VT* pv = reinterpret_cast<const VT*>(p);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int c = lane + RAE_WAVE * q;
+            v[q] = pv[c < nv ? c : 0];
+        }
+    }
+};
+
+template <int OPT>
+__device__ __forceinline__ void updv(float& p, float& ac, float g, float lr) {
+    p = opt_update<OPT>(p, &ac, g, lr);
+}
+template <int OPT>
+__device__ __forceinline__ void updv(float4& p, float4& ac, float4 g, float lr) {
+    p.x = opt_update<OPT>(p.x, &ac.x, g.x, lr);
+    p.y = opt_update<OPT>(p.y, &ac.y, g.y, lr);
+    p.z = opt_update<OPT>(p.z, &ac.z, g.z, lr);
+    p.w = opt_update<OPT>(p.w, &ac.w, g.w, lr);
+}
+
+template <int OPT, bool V4, int Q>
+__device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& pv,
+                                          RowVec<V4, Q>& av, const RowVec<V4, Q>& g, int nv,
+                                          float lr, int lane) {
+    typedef typename VecT<V4>::T VT;
+    VT* pp = reinterpret_cast<VT*>(p);
+    VT* aa = reinterpret_cast<VT*>(acc);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int c = lane + RAE_WAVE * q;
+        if (c < nv) {
+            updv<OPT>(pv.v[q], av.v[q], g.v[q], lr);
+            pp[c] = pv.v[q];
+            if (OPT == 0) aa[c] = av.v[q];
+        }
+    }
+}
+
+// ---- A / Ab rows -------------------------------------------------------------------------
+// g(A[e]) = sum over the row's records (in sorted order) of
+//   alpha_j * V1_b + beta_j * V2_b (+ X_b for j = 0 / Y_b for j = 1 when XY)
+// g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per record),
+// the record vectors RAE_UNR at a time with every load issued before the first FMA.
+template <int OPT, bool V4, int Q, bool XY>
+__device__ void task_entity_row(const StepArgs& a, int h, int u, int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    constexpr int UNR = Q == 1 ? 8 : 4;
+    typedef typename VecT<V4>::T VT;
+    const int r = a.r, nv = r / VW, NJ = 2 + 2 * a.s;
+    const int32_t* hdr = a.hdrA + 2 * h;
+    const int64_t base = (int64_t)h * a.RA;
+    const int e = a.urowA[base + u];
+    const int st = a.ustartA[base + u];
+    const int en = (u + 1 < hdr[1]) ? a.ustartA[base + u + 1] : hdr[0];
+    float* prow = a.A + (int64_t)e * r;
+    float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
+    RowVec<V4, Q> pv, av, g;
+    pv.load(prow, nv, lane);                     // parameters in flight with the records
+    if (OPT == 0) av.load(arow, nv, lane); else av.zero();
+    const float ab0 = a.Ab[e];
+    const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
+    g.zero();
+    float gb = 0.f;
+    for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
+        const int n = min(RAE_WAVE, en - c0);
+        const int rec = a.srecA[base + c0 + (lane < n ? lane : 0)];
+        const int b = rec / NJ, j = rec - b * NJ;
+        const float* er = a.ex + (int64_t)b * a.lay.rec + a.lay.ocoef + 3 * j;
+        float al = er[0], be = er[1];
+        const float ga = er[2];
+        if (lane >= n) al = be = 0.f;
+        gb += lane < n ? ga : 0.f;
+        const int xsel = XY ? (j == 0 ? a.lay.oX : a.lay.oY) : 0;
+        const float de = (XY && lane < n && j < 2) ? 1.f : 0.f;
+        for (int k0 = 0; k0 < n; k0 += UNR) {
+            VT v1[UNR][Q], v2[UNR][Q], v3[XY ? UNR : 1][Q];
+            float cal[UNR], cbe[UNR], cde[UNR];
+#pragma unroll
+            for (int k = 0; k < UNR; ++k) {
+                const int src = min(k0 + k, RAE_WAVE - 1);
+                const int bk = __shfl(b, src, 64);
+                cal[k] = (k0 + k < n) ? __shfl(al, src, 64) : 0.f;
+                cbe[k] = (k0 + k < n) ? __shfl(be, src, 64) : 0.f;
+                const float* rk = a.ex + (int64_t)bk * a.lay.rec;
+                const VT* V1 = reinterpret_cast<const VT*>(rk + a.lay.oV1);
+                const VT* V2 = reinterpret_cast<const VT*>(rk + a.lay.oV2);
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const int c = lane + RAE_WAVE * q;
+                    const int cs = c < nv ? c : 0;
+                    v1[k][q] = V1[cs];
+                    v2[k][q] = V2[cs];
+                }
+                if (XY) {
+                    cde[k] = (k0 + k < n) ? __shfl(de, src, 64) : 0.f;
+                    const int xk = __shfl(xsel, src, 64);
+                    const VT* V3 = reinterpret_cast<const VT*>(rk + xk);
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        const int c = lane + RAE_WAVE * q;
+                        v3[XY ? k : 0][q] = V3[c < nv ? c : 0];
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < UNR; ++k) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    vfma(g.v[q], cal[k], v1[k][q]);
+                    vfma(g.v[q], cbe[k], v2[k][q]);
+                    if (XY) vfma(g.v[q], cde[k], v3[XY ? k : 0][q]);
+                }
+            }
+        }
+    }
+    gb = wave_sum(gb);
+    apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+    if (lane == 0) {
+        float ac = aab0;
+        a.Ab[e] = opt_update<OPT>(ab0, &ac, gb, a.lr);
+        if (OPT == 0) a.aAb[e] = ac;
+    }
+}
+
+// ---- W rows: g(W[f]) = sum over the row's CSR records of x_bf * dS_b ----------------------
+template <int OPT, bool V4, int Q>
+__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int h, int u, int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    constexpr int UNR = Q == 1 ? 8 : 4;
+    typedef typename VecT<V4>::T VT;
+    const int m = a.m, nv = m / VW;
+    const int32_t* hdr = a.hdrW + 2 * h;
+    const int64_t base = (int64_t)h * a.RW;
+    const int f = a.urowW[base + u];
+    const int st = a.ustartW[base + u];
+    const int en = (u + 1 < hdr[1]) ? a.ustartW[base + u + 1] : hdr[0];
+    const unsigned mask = (1u << a.posbits) - 1u;
+    float* prow = a.W + (int64_t)f * m;
+    float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
+    RowVec<V4, Q> pv, av, g;
+    if (!a.reg_on) {
+        pv.load(prow, nv, lane);
+        if (OPT == 0) av.load(arow, nv, lane); else av.zero();
+    }
+    g.zero();
+    for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
+        const int n = min(RAE_WAVE, en - c0);
+        const unsigned rec = (unsigned)a.srecW[base + c0 + (lane < n ? lane : 0)];
+        const int b = (int)(rec >> a.posbits);
+        float val = 1.f;
+        if (a.values) val = a.values[a.indptr[ex0 + b] + (int)(rec & mask)];
+        if (lane >= n) val = 0.f;
+        for (int k0 = 0; k0 < n; k0 += UNR) {
+            VT v[UNR][Q];
+            float cv[UNR];
+#pragma unroll
+            for (int k = 0; k < UNR; ++k) {
+                const int src = min(k0 + k, RAE_WAVE - 1);
+                const int bk = __shfl(b, src, 64);
+                cv[k] = (k0 + k < n) ? __shfl(val, src, 64) : 0.f;
+                const VT* dS = reinterpret_cast<const VT*>(a.ex + (int64_t)bk * a.lay.rec + a.lay.odS);
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const int c = lane + RAE_WAVE * q;
+                    v[k][q] = dS[c < nv ? c : 0];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < UNR; ++k)
+#pragma unroll
+                for (int q = 0; q < Q; ++q) vfma(g.v[q], cv[k], v[k][q]);
+        }
+    }
+    if (a.reg_on) {
+        VT* gs = reinterpret_cast<VT*>(a.gWs + (int64_t)f * m);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int c = lane + RAE_WAVE * q;
+            if (c < nv) gs[c] = g.v[q];
+        }
+    } else {
+        apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
     }
 }
 

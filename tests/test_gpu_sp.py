@@ -165,3 +165,24 @@ def test_label_pass_matches_oracle(built_lib, cuda_dev):
     clear = (srt[:, -1] - srt[:, -2]) > 1e-4
     assert np.array_equal(lab.cpu().numpy()[clear], want_lab[clear])
     np.testing.assert_allclose(pr.cpu().numpy(), want_p, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", SP_CASES)
+def test_single_step_each_parameter(built_lib, cuda_dev, name):
+    """One func['train'] call: every parameter vs the reference's params after step 1."""
+    z, X = _case(name)
+    ind = _inducer(z, X, cuda_dev)
+    ind.compile_function()
+    l = int(z["l"])
+    c = ind.func["train"](0, z["neg1_e0"][:, :l], z["neg2_e0"][:, :l])
+    assert abs(c - float(z["costs"][0, 0])) <= COST_RTOL * max(1.0, abs(float(z["costs"][0, 0])))
+    got = _params(ind)
+    bad = []
+    for k in got:
+        err = np.abs(got[k] - z["step1_" + k])
+        tol = 1e-5 + 1e-4 * np.abs(z["step1_" + k])
+        if not np.all(err <= tol):
+            idx = np.unravel_index(np.argmax(err - tol), err.shape)
+            bad.append(f"{k}: max err {err.max():.3e} at {idx} got {got[k][idx]:.6g} "
+                       f"want {z['step1_' + k][idx]:.6g} init {z['init_' + k][idx]:.6g}")
+    assert not bad, "; ".join(bad)
