@@ -160,7 +160,8 @@ def main():
     st = torch.cuda.current_stream()
     sp_ = C.c_void_p(st.cuda_stream)
     b0 = W + K
-    n_it = min(args.kernel_iters, nb - b0)
+    n_it = min(args.kernel_iters, nb - b0, eng.index_window)
+    lib.rae_build_index(plan, b0, n_it, sp_)
     lib.rae_set_cursor(plan, b0, sp_)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
             torch.cuda.Event(enable_timing=True)) for _ in range(n_it)]

@@ -78,6 +78,7 @@ typedef struct rae_config {
     int32_t max_row_nnz;      /* max nnz of one example row                               */
     int32_t neg_mode;         /* RAE_NEG_*                                                */
     int64_t neg_stride;       /* row stride (elements) of the neg arrays                  */
+    int64_t index_window;     /* batches whose row index is held at once (0 = default)   */
 } rae_config;
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
@@ -124,19 +125,27 @@ int64_t rae_exchange_floats(const rae_config* cfg);
 int rae_set_negatives(rae_plan* plan, const int32_t* neg1_dev, const int32_t* neg2_dev,
                       int32_t mode, int64_t stride);
 
+/* --- the row index ----------------------------------------------------------------- */
+/* Build the per-batch row index (for every parameter row a batch references, its
+ * contributing records in a fixed order) for global batches [first, first+count), from the
+ * current negatives; count <= rae_index_window().  Batch b uses slot b % window, so build
+ * a window before stepping through it.  Independent of the parameters. */
+int rae_build_index(rae_plan* plan, int64_t first_batch, int64_t count, rae_stream_t stream);
+int64_t rae_index_window(rae_plan* plan);
+
 /* --- the training step (func['train']) --------------------------------------------- */
 /* Batch addressed as  batch = *cursor + step_offset  (cursor: device int64 owned by the
  * plan) so a captured sequence of steps can be replayed for successive batches.        */
 int rae_set_cursor(rae_plan* plan, int64_t batch, rae_stream_t stream);
 int rae_advance_cursor(rae_plan* plan, int64_t count, rae_stream_t stream);
-/* K1: per-example encoder + decoder forward/backward of this rank's l examples, plus the
- * per-step row index of the global batch.  Writes the exchange records.                  */
+/* K1: per-example encoder + decoder forward/backward of this rank's l examples.  Writes the
+ * exchange records.  The batch's row index must have been built (rae_build_index).      */
 int rae_step_forward(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
 /* K2 (+K3 when lambda1/lambda2 != 0): deterministic per-row gradient reduction over the
  * global batch and the optimizer update of every parameter; writes costs[batch].        */
 int rae_step_update(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
 /* One whole func['train'](batch_index, neg1, neg2) call on a single rank:
- * rae_set_negatives(PER_CALL) + forward + update for `batch_index`.                    */
+ * rae_set_negatives(PER_CALL) + index + forward + update for `batch_index`.            */
 int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,
                    const int32_t* neg2_dev, rae_stream_t stream);
 /* Device error word (overflow flags); host reads it with rae_check(). */

@@ -31,22 +31,26 @@ using namespace rae;
 // ======================================================================================
 // kernels
 // ======================================================================================
-template <int DEC, bool V4>
-__global__ __launch_bounds__(RAE_FBT) void k_forward(StepArgs a) {
+template <int DEC, bool V4, class D>
+__global__ __launch_bounds__(RAE_FBT) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = *a.cursor + a.step_offset;
-    const int bid = blockIdx.x;
-    if (bid < a.HA) {
-        build_index_partition<RAE_FBT>(a, g, true, bid, smem);
-        return;
-    }
-    if (bid < a.HA + a.HW) {
-        build_index_partition<RAE_FBT>(a, g, false, bid - a.HA, smem);
-        return;
-    }
-    const int bl = bid - a.HA - a.HW;
-    if (DEC == RAE_DEC_SP) sp_example<V4, V4>(a, g, bl, smem);
-    else bilinear_example<V4>(a, g, bl, smem, DEC == RAE_DEC_HYBRID);
+    if (DEC == RAE_DEC_SP) sp_example<V4, D>(a, g, blockIdx.x, smem);
+    else bilinear_example<V4>(a, g, blockIdx.x, smem, DEC == RAE_DEC_HYBRID);
+}
+
+// shapes with compile-time specialisations of the forward kernel (BASELINE.json configs
+// C3/C5: K=100 r=200 s=20; C2: K=30 r=100 s=10); every other shape runs the runtime-shape
+// instantiation of the same code
+typedef FixDims<100, 200, 20> DimsC3;
+typedef FixDims<30, 100, 10> DimsC2;
+
+// row index of global batches [first, first + gridDim.x): blockIdx.y 0 -> A/Ab, 1 -> W
+__global__ __launch_bounds__(RAE_FBT) void k_build_index(StepArgs a, int64_t first) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t g = first + blockIdx.x;
+    build_batch_index<RAE_FBT>(a, g, g % a.index_window, blockIdx.y == 0, smem);
 }
 
 __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
@@ -55,6 +59,16 @@ __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
 __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
     return dec != RAE_DEC_SP ? ((r * r + 15) / 16) * ((m + 15) / 16) : 0;
 }
+
+#ifdef RAE_STAMPS
+#define RAE_WAVE_END()                                                                      \
+    do {                                                                                    \
+        if (a.stamps && lane == 0 && t == gw)                                               \
+            a.stamps[(size_t)gw * 4 + 2] = __builtin_amdgcn_s_memrealtime();                 \
+    } while (0)
+#else
+#define RAE_WAVE_END() do { } while (0)
+#endif
 
 template <int OPT, bool V4, int Q, bool BIL>
 __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
@@ -66,44 +80,63 @@ __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
     const int nCt = n_ctiles(a.dec, a.r, a.m);
     const int nRt = n_rtiles(a.dec, a.r, a.m);
-    const int TA = total_rows(a.hdrA, a.HA);
-    const int TW = total_rows(a.hdrW, a.HW);
+    const int64_t slot = g % a.index_window;
+    const int CA = a.hdrA[2 * slot], TA = a.hdrA[2 * slot + 1];
+    const int CW = a.hdrW[2 * slot], TW = a.hdrW[2 * slot + 1];
     const int T = nCt + nRt + mt + 1 + TA + TW;
+#ifdef RAE_STAMPS
+    unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    int first_type = -1;
+#endif
     for (int t = gw; t < T; t += nw) {
         int tt = t;
+#ifdef RAE_STAMPS
+        if (first_type < 0) {
+            first_type = t < nCt ? 0 : (t < nCt + nRt ? 1 : (t < nCt + nRt + mt ? 2 :
+                         (t < nCt + nRt + mt + 1 ? 3 : (t < nCt + nRt + mt + 1 + TA ? 4 : 5))));
+            if (a.stamps && lane == 0) {
+                a.stamps[(size_t)gw * 4 + 0] = t_start;
+                a.stamps[(size_t)gw * 4 + 1] = (unsigned long long)first_type;
+            }
+        }
+#endif
         if (tt < nCt) {
             const int which = tt / (rt * mt), ti = tt - which * rt * mt;
             task_mfma_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
                                 which ? a.lay.odw2 : a.lay.odw1, false, (ti / mt) * 16,
                                 (ti % mt) * 16, t, lane);
+            RAE_WAVE_END();
             continue;
         }
         tt -= nCt;
         if (BIL && tt < nRt) {
             task_bilinear_tile<OPT>(a, (tt / mt) * 16, (tt % mt) * 16, nCt + tt, lane);
+            RAE_WAVE_END();
             continue;
         }
         tt -= nRt;
         if (tt < mt) {
             task_mfma_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, tt * 16, 0, lane);
+            RAE_WAVE_END();
             continue;
         }
         tt -= mt;
         if (tt == 0) {
             task_cost(a, lane);
+            RAE_WAVE_END();
             continue;
         }
         tt -= 1;
         if (tt < TA) {
-            int u;
-            const int h = locate_row(a.hdrA, a.HA, tt, &u);
-            task_entity_row<OPT, V4, Q, BIL>(a, h, u, lane);
+            task_entity_row<OPT, V4, Q, BIL>(a, slot, tt, TA, CA, lane);
+            RAE_WAVE_END();
             continue;
         }
         tt -= TA;
-        int u;
-        const int h = locate_row(a.hdrW, a.HW, tt, &u);
-        task_feature_row<OPT, V4, Q>(a, ex0, h, u, lane);
+        task_feature_row<OPT, V4, Q>(a, ex0, slot, tt, TW, CW, lane);
+#ifdef RAE_STAMPS
+        if (a.stamps && lane == 0 && t == gw) a.stamps[(size_t)gw * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 
@@ -251,9 +284,12 @@ struct rae_plan {
     int* d_err = nullptr;
     char* ws = nullptr;
     size_t smem_fwd = 0;
+    size_t smem_idx = 0;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
     int q = 1;
+    unsigned long long* stamps_fwd = nullptr;
+    unsigned long long* stamps_upd = nullptr;
 };
 
 extern "C" const char* rae_last_error(void) { return g_last_error.c_str(); }
@@ -356,8 +392,14 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // row-index partitions: ~1024 records per partition on average, LDS holds RAE_KCAP
     a.RA = L * NJ;
     a.RW = c.max_batch_nnz > 0 ? c.max_batch_nnz : 1;
-    a.HA = ceil_div(a.RA, RAE_PART);
-    a.HW = ceil_div(a.RW, RAE_PART);
+    a.HA = index_partitions(a.RA);
+    a.HW = index_partitions(a.RW);
+    {
+        const int64_t nb = c.n_examples / L;
+        int64_t win = c.index_window > 0 ? c.index_window : 2048;
+        if (win > nb) win = nb;
+        a.index_window = win < 1 ? 1 : win;
+    }
     int bbits = 1;
     while ((1 << bbits) < L) ++bbits;
     a.posbits = 31 - bbits;
@@ -378,11 +420,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return o;
     };
     const size_t o_cursor = take(8), o_zero = take(8), o_err = take(8), o_base = take(8);
-    const size_t o_hdrA = take(8 * a.HA), o_hdrW = take(8 * a.HW);
-    const size_t o_srecA = take(4ull * a.HA * a.RA), o_urowA = take(4ull * a.HA * a.RA),
-                 o_ustA = take(4ull * a.HA * a.RA);
-    const size_t o_srecW = take(4ull * a.HW * a.RW), o_urowW = take(4ull * a.HW * a.RW),
-                 o_ustW = take(4ull * a.HW * a.RW);
+    const size_t W_ = (size_t)a.index_window;
+    const size_t o_hdrA = take(8 * W_), o_hdrW = take(8 * W_);
+    const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(8ull * W_ * a.RA);
+    const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(8ull * W_ * a.RW);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
@@ -399,10 +440,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.hdrW = reinterpret_cast<int32_t*>(p->ws + o_hdrW);
     a.srecA = reinterpret_cast<int32_t*>(p->ws + o_srecA);
     a.urowA = reinterpret_cast<int32_t*>(p->ws + o_urowA);
-    a.ustartA = reinterpret_cast<int32_t*>(p->ws + o_ustA);
+
     a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
-    a.ustartW = reinterpret_cast<int32_t*>(p->ws + o_ustW);
+
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
     a.err = p->d_err;
@@ -410,27 +451,31 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    const size_t smem_idx = 8ull * RAE_KCAP + 4ull * (33 + L + 1);
-    p->smem_fwd = smem_ex > smem_idx ? smem_ex : smem_idx;
-    if (p->smem_fwd > 160 * 1024) {
+    p->smem_idx = 8ull * RAE_KCAP + 4ull * (33 + L + 1);
+    p->smem_fwd = smem_ex;
+    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024) {
         (void)hipFree(p->ws);
         delete p;
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
     }
-    p->grid_fwd = a.HA + a.HW + c.batch_size;
-    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + (c.relations + 15) / 16 + 1;
+    p->grid_fwd = c.batch_size;
+    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + (c.relations + 15) / 16 + 1;  // upper bound
     int gu = ceil_div(tasks, RAE_NWAVE);
     p->grid_update = gu < 1 ? 1 : (gu > 8192 ? 8192 : gu);
     {
-        const void* fns[] = {(const void*)k_forward<RAE_DEC_SP, true>,
-                             (const void*)k_forward<RAE_DEC_SP, false>,
-                             (const void*)k_forward<RAE_DEC_RESCAL, true>,
-                             (const void*)k_forward<RAE_DEC_RESCAL, false>,
-                             (const void*)k_forward<RAE_DEC_HYBRID, true>,
-                             (const void*)k_forward<RAE_DEC_HYBRID, false>};
+        const void* fns[] = {(const void*)k_forward<RAE_DEC_SP, true, DimsC3>,
+                             (const void*)k_forward<RAE_DEC_SP, false, DimsC2>,
+                             (const void*)k_forward<RAE_DEC_SP, true, DynDims>,
+                             (const void*)k_forward<RAE_DEC_SP, false, DynDims>,
+                             (const void*)k_forward<RAE_DEC_RESCAL, true, DynDims>,
+                             (const void*)k_forward<RAE_DEC_RESCAL, false, DynDims>,
+                             (const void*)k_forward<RAE_DEC_HYBRID, true, DynDims>,
+                             (const void*)k_forward<RAE_DEC_HYBRID, false, DynDims>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p->smem_fwd);
+        (void)hipFuncSetAttribute((const void*)k_build_index,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
     }
     *out = p;
     return RAE_OK;
@@ -470,10 +515,23 @@ extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t strea
 
 template <int DEC>
 static void launch_fwd_dec(rae_plan* p, const StepArgs& a, hipStream_t st) {
+    const dim3 gr(p->grid_fwd), bt(RAE_FBT);
+    const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;
+    const bool c2 = a.m == 30 && a.r == 100 && a.s == 10;
+    if constexpr (DEC == RAE_DEC_SP) {
+        if (c3 && p->v4) {
+            hipLaunchKernelGGL((k_forward<DEC, true, DimsC3>), gr, bt, p->smem_fwd, st, a);
+            return;
+        }
+        if (c2 && !p->v4) {
+            hipLaunchKernelGGL((k_forward<DEC, false, DimsC2>), gr, bt, p->smem_fwd, st, a);
+            return;
+        }
+    }
     if (p->v4)
-        hipLaunchKernelGGL((k_forward<DEC, true>), dim3(p->grid_fwd), dim3(RAE_FBT), p->smem_fwd, st, a);
+        hipLaunchKernelGGL((k_forward<DEC, true, DynDims>), gr, bt, p->smem_fwd, st, a);
     else
-        hipLaunchKernelGGL((k_forward<DEC, false>), dim3(p->grid_fwd), dim3(RAE_FBT), p->smem_fwd, st, a);
+        hipLaunchKernelGGL((k_forward<DEC, false, DynDims>), gr, bt, p->smem_fwd, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
@@ -481,6 +539,7 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     StepArgs a = p->args;
     a.cursor = cursor;
     a.step_offset = off;
+    a.stamps = p->stamps_fwd;
     switch (a.dec) {
         case RAE_DEC_SP: launch_fwd_dec<RAE_DEC_SP>(p, a, st); break;
         case RAE_DEC_RESCAL: launch_fwd_dec<RAE_DEC_RESCAL>(p, a, st); break;
@@ -510,6 +569,7 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     StepArgs a = p->args;
     a.cursor = cursor;
     a.step_offset = off;
+    a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
     if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
     else launch_update_q<1>(p, gu, bt, st, a);
@@ -525,6 +585,26 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     }
     return RAE_OK;
 }
+
+static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t st) {
+    if (!p->args.neg1 || !p->args.neg2) return fail(RAE_E_STATE, "negatives not set");
+    const int64_t nb = p->cfg.n_examples / ((int64_t)p->cfg.batch_size * p->cfg.world_size);
+    if (first < 0 || count < 0 || first + count > nb)
+        return fail(RAE_E_INVALID, "batch range out of the epoch");
+    if (count > p->args.index_window)
+        return fail(RAE_E_INVALID, "more batches than the index window holds");
+    if (count == 0) return RAE_OK;
+    hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 2), dim3(RAE_FBT), p->smem_idx, st,
+                       p->args, first);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+
+extern "C" int rae_build_index(rae_plan* p, int64_t first, int64_t count, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    return launch_index(p, first, count, (hipStream_t)stream);
+}
+extern "C" int64_t rae_index_window(rae_plan* p) { return p ? p->args.index_window : -1; }
 
 extern "C" int rae_step_forward(rae_plan* p, int64_t off, rae_stream_t stream) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
@@ -544,10 +624,27 @@ extern "C" int rae_train_step(rae_plan* p, int64_t batch, const int32_t* n1, con
     if (batch < 0 || batch >= nb) return fail(RAE_E_INVALID, "batch index out of range");
     int rc = rae_set_negatives(p, n1, n2, RAE_NEG_PER_CALL, p->cfg.batch_size);
     if (rc) return rc;
+    rc = launch_index(p, batch, 1, (hipStream_t)stream);
+    if (rc) return rc;
     rc = launch_forward(p, p->d_zero, batch, (hipStream_t)stream);
     if (rc) return rc;
     return launch_update(p, p->d_zero, batch, (hipStream_t)stream);
 }
+
+#ifdef RAE_STAMPS
+// diagnostic build only: point the kernels at a stamp buffer (16 u64 per forward block,
+// 4 u64 per update wave); fwd=1 -> forward launches, fwd=0 -> update launches
+extern "C" int rae_debug_stamps(rae_plan* p, unsigned long long* buf, int fwd) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    p->stamps_fwd = fwd ? buf : nullptr;
+    p->stamps_upd = fwd ? nullptr : buf;
+    return RAE_OK;
+}
+extern "C" int rae_debug_grid(rae_plan* p, int* out) {
+    out[0] = p->grid_fwd; out[1] = p->grid_update; out[2] = 0; out[3] = 0;
+    return RAE_OK;
+}
+#endif
 
 extern "C" int rae_check(rae_plan* p) {
     if (!p) return fail(RAE_E_INVALID, "null plan");

@@ -12,11 +12,70 @@
 
 namespace rae {
 
-// xor-butterfly all-reduce: every lane ends with the bitwise-identical sum (fp add is
-// commutative, so partner lanes compute a+b and b+a identically).
+// ---- cross-lane primitives (VALU DPP + gfx950 permlane swaps; no LDS round trip) -------
+// DPP controls: quad_perm [1,0,3,2] = 0xB1 (lane^1), [2,3,0,1] = 0x4E (lane^2),
+// row_half_mirror = 0x141 (within 8: i <-> 7-i), row_mirror = 0x140 (within 16: i <-> 15-i),
+// row_shl:n = 0x100+n (lane i <- i+n), row_shr:n = 0x110+n (lane i <- i-n).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL,
+                                                      0xF, 0xF, false));
+}
+// value of lane (lane ^ 16) / (lane ^ 32) via v_permlane16_swap / v_permlane32_swap
+__device__ __forceinline__ unsigned xor16_u32(unsigned v) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? p[0] : p[1];
+}
+__device__ __forceinline__ unsigned xor32_u32(unsigned v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? p[0] : p[1];
+}
+// value of lane (lane ^ j) for j = 1..32 (j wave-uniform)
+__device__ __forceinline__ unsigned xor_lane_u32(unsigned v, int j) {
+    const int lane = threadIdx.x & 63;
+    switch (j) {
+        case 1: return dpp_u32<0xB1>(v);
+        case 2: return dpp_u32<0x4E>(v);
+        case 4: { const unsigned a = dpp_u32<0x104>(v), b = dpp_u32<0x114>(v);
+                  return (lane & 4) ? b : a; }
+        case 8: { const unsigned a = dpp_u32<0x108>(v), b = dpp_u32<0x118>(v);
+                  return (lane & 8) ? b : a; }
+        case 16: return xor16_u32(v);
+        default: return xor32_u32(v);
+    }
+}
+__device__ __forceinline__ unsigned long long xor_lane_u64(unsigned long long v, int j) {
+    const unsigned lo = xor_lane_u32((unsigned)(v & 0xffffffffull), j);
+    const unsigned hi = xor_lane_u32((unsigned)(v >> 32), j);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// sum over the 16 lanes of a lane group; every lane of the group gets the identical value
+// (each step adds two commuted operands, so partner lanes compute bitwise-equal sums)
+__device__ __forceinline__ float group16_sum(float v) {
+    v += dpp_f32<0xB1>(v);
+    v += dpp_f32<0x4E>(v);
+    v += dpp_f32<0x141>(v);
+    v += dpp_f32<0x140>(v);
+    return v;
+}
+// wave-wide all-reduce sum, identical in every lane, fixed order -> deterministic
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = group16_sum(v);
+    {
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                        false, false);
+        v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+    {
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                        false, false);
+        v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
     return v;
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -25,22 +84,16 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-// sum over the 16 lanes of a lane group (lane & ~15 fixed)
-__device__ __forceinline__ float group16_sum(float v) {
-    v += __shfl_xor(v, 8, 16);
-    v += __shfl_xor(v, 4, 16);
-    v += __shfl_xor(v, 2, 16);
-    v += __shfl_xor(v, 1, 16);
+    v = fmaxf(v, dpp_f32<0xB1>(v));
+    v = fmaxf(v, dpp_f32<0x4E>(v));
+    v = fmaxf(v, dpp_f32<0x141>(v));
+    v = fmaxf(v, dpp_f32<0x140>(v));
+    v = fmaxf(v, __uint_as_float(xor16_u32(__float_as_uint(v))));
+    v = fmaxf(v, __uint_as_float(xor32_u32(__float_as_uint(v))));
     return v;
 }
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
-    const unsigned lo = __shfl_xor((unsigned)(v & 0xffffffffull), o, 64);
-    const unsigned hi = __shfl_xor((unsigned)(v >> 32), o, 64);
-    return ((unsigned long long)hi << 32) | lo;
+    return xor_lane_u64(v, o);
 }
 
 // Block-wide sum / max for BT threads; `red` is >= BT/64 floats of LDS.

@@ -12,13 +12,15 @@
 //   scores = [logsig(u), H, H, logsig(-g)]             :39,49-50
 //   cost = -mean(scores)                               OieModel.py:90
 // and its analytic backward (the reference uses T.grad, Optimizers.py:27).
-// Outputs: the exchange record (rae_step.hpp); nothing is scattered here -- the row
+// Output: the exchange record (rae_step.hpp); nothing is scattered here -- the row
 // gradients are formed deterministically in the update kernel from these records.
 //
-// Latency structure (the step is ~100 examples, so each example's dependent memory round
-// trips ARE the kernel time): C1/C2 are loaded once into registers at kernel entry (both
-// matvecs use them), the A-row gather is issued before the encoder and stored to LDS
-// after it, and the encoder spreads the feature-row gathers over all threads.
+// The step is ~100 examples, so one example's dependent memory round trips and its
+// instruction issue ARE the kernel time.  Hence: dimensions are compile-time for the
+// BASELINE shapes (FixDims; DynDims is the runtime-shape fallback), C1/C2 are held in
+// registers and serve both matvecs, the A rows arrive by LDS-DMA while the W rows load,
+// softmax / coefficient work runs in one wave without barriers, and every cross-lane
+// reduction is DPP / permlane (VALU), not LDS.
 #pragma once
 #include "rae_common.hpp"
 #include "rae_step.hpp"
@@ -27,8 +29,23 @@ namespace rae {
 
 #define RAE_FNW (RAE_FBT / RAE_WAVE)     // waves per forward workgroup
 #define RAE_NG (RAE_FBT / 16)            // 16-lane groups per forward workgroup
-#define RAE_CRA 7                        // C rows cached per lane group (r <= 7*32 = 224)
-#define RAE_CCC 2                        // C column vectors cached per lane (<= 32 vectors)
+
+// ---- compile-time or runtime shapes ------------------------------------------------------
+struct DynDims {
+    int m, r, s;
+    __device__ explicit DynDims(const StepArgs& a) : m(a.m), r(a.r), s(a.s) {}
+    static constexpr bool fixed = false;
+};
+template <int M, int R, int S>
+struct FixDims {
+    static constexpr int m = M, r = R, s = S;
+    __device__ explicit FixDims(const StepArgs&) {}
+    static constexpr bool fixed = true;
+};
+
+// compile-time extents (0 for runtime shapes)
+template <class D> struct DimT { static constexpr int m = 0, r = 0; };
+template <int M, int R, int S> struct DimT<FixDims<M, R, S>> { static constexpr int m = M, r = R; };
 
 struct ExampleSmem {
     float *sP, *slogP, *sdP, *swC1, *swC2, *sdw1, *sdw2, *srows, *sdots, *sAbv, *scoef,
@@ -36,11 +53,16 @@ struct ExampleSmem {
     int *sfidx, *sids, *sint;
 };
 
+// P / logP / dP regions are padded to a multiple of 64 vectors so the register-cache
+// matvecs may read past m (the padding holds zeros)
+__host__ __device__ inline int pad_m(int m) { return ((m + 255) / 256) * 256; }
+
 __host__ __device__ inline int example_smem_floats(int dec, int m, int r, int s) {
-    const int m4 = align4(m), r4 = align4(r), NJ = 2 + 2 * s, NJ4 = align4(NJ);
+    const int mp = pad_m(m), r4 = align4(r), NJ = 2 + 2 * s, NJ4 = align4(NJ);
     const int NR = (dec == 0) ? 1 + 2 * s : 2 + 2 * s;
-    const int partf = (RAE_FNW * m4 > RAE_FBT * 4 + 4) ? RAE_FNW * m4 : RAE_FBT * 4 + 4;
-    int f = 3 * m4 + 4 * r4 + NR * r4 + 2 * NJ4 + align4(3 * NJ) + 64 + partf +
+    int partf = (RAE_FNW * mp > RAE_FBT * 4) ? RAE_FNW * mp : RAE_FBT * 4;
+    if (16 * r4 > partf) partf = 16 * r4;
+    int f = 3 * mp + 4 * r4 + NR * r4 + 2 * NJ4 + align4(3 * NJ) + 64 + partf +
             2 * RAE_FBT + NJ4 + 16;
     if (dec != 0) f += 3 * r4 + 4 * r4;
     return f;
@@ -48,13 +70,14 @@ __host__ __device__ inline int example_smem_floats(int dec, int m, int r, int s)
 
 __device__ inline ExampleSmem carve_example_smem(char* smem, int dec, int m, int r, int s) {
     ExampleSmem S;
-    const int m4 = align4(m), r4 = align4(r), NJ = 2 + 2 * s, NJ4 = align4(NJ);
+    const int mp = pad_m(m), r4 = align4(r), NJ = 2 + 2 * s, NJ4 = align4(NJ);
     const int NR = (dec == 0) ? 1 + 2 * s : 2 + 2 * s;
-    const int partf = (RAE_FNW * m4 > RAE_FBT * 4 + 4) ? RAE_FNW * m4 : RAE_FBT * 4 + 4;
+    int partf = (RAE_FNW * mp > RAE_FBT * 4) ? RAE_FNW * mp : RAE_FBT * 4;
+    if (16 * r4 > partf) partf = 16 * r4;
     float* p = reinterpret_cast<float*>(smem);
-    S.sP = p; p += m4;
-    S.slogP = p; p += m4;
-    S.sdP = p; p += m4;
+    S.sP = p; p += mp;
+    S.slogP = p; p += mp;
+    S.sdP = p; p += mp;
     S.swC1 = p; p += r4;
     S.swC2 = p; p += r4;
     S.sdw1 = p; p += r4;
@@ -81,37 +104,38 @@ __device__ inline ExampleSmem carve_example_smem(char* smem, int dec, int m, int
 
 // ---- shared pieces of every decoder's example path --------------------------------------
 
-// ids of the NJ records (e1, e2, neg1[t], neg2[t]), feature range; Ab after a barrier
-__device__ __forceinline__ void load_ids(const StepArgs& a, int64_t ex, int64_t col,
+// ids of the NJ records (e1, e2, neg1[t], neg2[t]) and the feature range
+template <class D>
+__device__ __forceinline__ void load_ids(const StepArgs& a, const D& Dm, int64_t ex, int64_t col,
                                          ExampleSmem& S) {
-    const int NJ = 2 + 2 * a.s;
-    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
-        int id;
-        if (j == 0) id = a.args1[ex];
-        else if (j == 1) id = a.args2[ex];
-        else if (j < 2 + a.s) id = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
-        else id = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
-        S.sids[j] = id;
+    const int NJ = 2 + 2 * Dm.s;
+    const int j = threadIdx.x;
+    if (j < NJ) {
+        const int* src = (j == 0) ? a.args1 + ex
+                       : (j == 1) ? a.args2 + ex
+                       : (j < 2 + Dm.s) ? a.neg1 + (int64_t)(j - 2) * a.neg_stride + col
+                                        : a.neg2 + (int64_t)(j - 2 - Dm.s) * a.neg_stride + col;
+        S.sids[j] = *src;
     }
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == RAE_FBT - 1) {
         S.sint[0] = a.indptr[ex];
         S.sint[1] = a.indptr[ex + 1];
     }
 }
 
-// A-row gather straight into LDS with LDS-DMA (global_load_lds: no VGPR staging, the
-// copy proceeds asynchronously until the next barrier).  Row rho -> record j (SP skips e2:
-// j = rho ? rho+1 : 0; bilinear j = rho).  One wave instruction moves 64 lanes x 16 B
-// (V4) or 64 x 4 B; the LDS destination is the wave-uniform row base + lane*size.
+// A-row gather straight into LDS with LDS-DMA (global_load_lds: no VGPR staging; the copy
+// lands while the W rows load).  Row rho -> record j (SP skips e2: j = rho ? rho+1 : 0;
+// bilinear j = rho).  One wave instruction moves 64 lanes x 16 B (V4) or 64 x 4 B; the LDS
+// destination is the wave-uniform row base + lane*size.
 typedef __attribute__((address_space(3))) void rae_lds_void;
 typedef __attribute__((address_space(1))) void rae_glob_void;
 
-template <bool V4>
-__device__ __forceinline__ void gather_rows_dma(const StepArgs& a, ExampleSmem& S, int NR,
-                                                int skip_e2) {
+template <bool V4, class D>
+__device__ __forceinline__ void gather_rows_dma(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                                int NR, int skip_e2) {
     constexpr int VW = V4 ? 4 : 1;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int rv = a.r / VW, r4 = align4(a.r);
+    const int rv = Dm.r / VW, r4 = align4(Dm.r);
     const int nchunk = (rv + 63) / 64;
     for (int t = w; t < NR * nchunk; t += RAE_FNW) {
         const int rho = t / nchunk, ch = t - rho * nchunk;
@@ -119,7 +143,7 @@ __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, ExampleSmem& 
         const int c = ch * 64 + lane;
         float* dst = S.srows + rho * r4 + ch * 64 * VW;
         if (c < rv) {
-            const float* src = a.A + (int64_t)S.sids[j] * a.r + (int64_t)c * VW;
+            const float* src = a.A + (int64_t)S.sids[j] * Dm.r + (int64_t)c * VW;
             if constexpr (V4)
                 __builtin_amdgcn_global_load_lds((rae_glob_void*)src, (rae_lds_void*)dst, 16, 0, 0);
             else
@@ -128,137 +152,72 @@ __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, ExampleSmem& 
     }
 }
 
-// S = X.W + Wb over all threads (slot = feature lane group), softmax, entropy.
-// Returns H (alpha-scaled) in all threads.  V4 requires m % 4 == 0.
-template <bool V4, bool V4R>
-__device__ __forceinline__ float encoder_forward(const StepArgs& a, ExampleSmem& S, int NR,
-                                                 int skip_e2) {
-    typedef typename VecT<V4>::T VT;
-    constexpr int VW = V4 ? 4 : 1;
-    const int m = a.m, mv = m / VW;
-    const int p0 = S.sint[0], p1 = S.sint[1];
-    const int nslot = RAE_FBT / mv > 0 ? RAE_FBT / mv : 1;
-    const int slot = threadIdx.x / mv, c = threadIdx.x - slot * mv;
-    const VT* Wv = reinterpret_cast<const VT*>(a.W);
-    VT acc;
-    vzero(acc);
-    for (int pc = p0; pc < p1; pc += RAE_FBT) {
-        const int nf = min(RAE_FBT, p1 - pc);
-        __syncthreads();
-        if (threadIdx.x < nf) {
-            S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
-            S.sfval[threadIdx.x] = a.values ? a.values[pc + threadIdx.x] : 1.f;
-        }
-        __syncthreads();
-        if (pc == p0) gather_rows_dma<V4R>(a, S, NR, skip_e2);   // overlaps the W-row loads
-        if (slot < nslot) {
-            for (int cc = c; cc < mv; cc += RAE_FBT) {      // mv > RAE_FBT only for huge m
-                for (int f = slot; f < nf; f += nslot)
-                    vfma(acc, S.sfval[f], Wv[(int64_t)S.sfidx[f] * mv + cc]);
-            }
-        }
-    }
-    if (p1 <= p0) gather_rows_dma<V4R>(a, S, NR, skip_e2);      // no features
-    // combine slots in fixed order
-    VT* part = reinterpret_cast<VT*>(S.spart);
-    if (slot < nslot && mv <= RAE_FBT) part[slot * mv + c] = acc;
-    __syncthreads();
-    float* sS = S.sdP;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-        float v = 0.f;
-        for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
-        sS[k] = v + a.Wb[k];
-    }
-    __syncthreads();
-    float mx = -INFINITY;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) mx = fmaxf(mx, sS[k]);
-    mx = block_max<RAE_FBT>(mx, S.sred);
-    float se = 0.f;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) se += expf(sS[k] - mx);
-    se = block_sum<RAE_FBT>(se, S.sred + 8);
-    const float lse = logf(se);
-    float hp = 0.f;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-        const float lp = (sS[k] - mx) - lse;
-        const float p = expf(sS[k] - mx) / se;
-        S.slogP[k] = lp;
-        S.sP[k] = p;
-        hp += p * lp;
-    }
-    hp = block_sum<RAE_FBT>(hp, S.sred + 16);
-    return -a.alpha * hp;
-}
-
-// Register cache of C1, C2 (row-major (r, m)) in the lane-group layout:
-// group gid (16 lanes) owns rows i = r0 + gid + NG*ra, lane q owns column vectors
-// c = c0 + q + 16*cc.  When the whole matrix fits (r <= NG*RAE_CRA, m/VW <= 16*RAE_CCC) it is
-// loaded once and serves both matvecs; otherwise chunks are (re)loaded from L2.
-template <bool V4>
+// ---- decoder weight matrices C1, C2 (r, m) in registers ----------------------------------
+// group gid (16 lanes) owns rows i = gid + NG*ra, lane q owns column vectors c = q + 16*cc.
+// Fixed shapes that fit keep the whole pair resident for both matvecs; otherwise the
+// matrices stream through the same registers chunk by chunk.
+template <bool V4, class D>
 struct CCache {
     typedef typename VecT<V4>::T VT;
-    VT c1[RAE_CRA][RAE_CCC], c2[RAE_CRA][RAE_CCC];
+    static constexpr int VW = V4 ? 4 : 1;
+    static constexpr int RA0 = D::fixed ? (DimT<D>::r + RAE_NG - 1) / RAE_NG : 7;
+    static constexpr int CC0 = D::fixed ? (DimT<D>::m / VW + 15) / 16 : 2;
+    static constexpr bool FITS = D::fixed && RA0 <= 7 && CC0 <= 2;
+    static constexpr int RA = FITS ? RA0 : 7;
+    static constexpr int CC = FITS ? CC0 : 2;
+    VT c1[RA][CC], c2[RA][CC];
 
-    __device__ __forceinline__ void load(const float* C1, const float* C2, int r, int mv, int r0,
-                                         int c0) {
-        const VT* C1v = reinterpret_cast<const VT*>(C1);
-        const VT* C2v = reinterpret_cast<const VT*>(C2);
+    // branch-free: out-of-range rows/columns load a clamped (valid) element; their
+    // contributions are multiplied by zero-padded P / zeroed dw
+    __device__ __forceinline__ void load(const StepArgs& a, const D& Dm, int r0, int c0) {
+        const VT* C1v = reinterpret_cast<const VT*>(a.C1);
+        const VT* C2v = reinterpret_cast<const VT*>(a.C2);
+        const int mv = Dm.m / VW;
         const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
 #pragma unroll
-        for (int ra = 0; ra < RAE_CRA; ++ra) {
-            const int i = r0 + gid + RAE_NG * ra;
+        for (int ra = 0; ra < RA; ++ra) {
+            const int i = min(r0 + gid + RAE_NG * ra, Dm.r - 1);
 #pragma unroll
-            for (int cc = 0; cc < RAE_CCC; ++cc) {
-                const int c = c0 + q + 16 * cc;
-                if (i < r && c < mv) {
-                    c1[ra][cc] = C1v[(int64_t)i * mv + c];
-                    c2[ra][cc] = C2v[(int64_t)i * mv + c];
-                } else {
-                    vzero(c1[ra][cc]);
-                    vzero(c2[ra][cc]);
-                }
+            for (int cc = 0; cc < CC; ++cc) {
+                const int c = min(c0 + q + 16 * cc, mv - 1);
+                c1[ra][cc] = C1v[i * mv + c];
+                c2[ra][cc] = C2v[i * mv + c];
             }
         }
     }
 };
 
-__host__ __device__ inline bool ccache_fits(int r, int mv) {
-    return r <= RAE_NG * RAE_CRA && mv <= 16 * RAE_CCC;
-}
-
 // wC1 = C1.P, wC2 = C2.P  -> S.swC1, S.swC2
-template <bool V4>
-__device__ __forceinline__ void sp_project(const StepArgs& a, ExampleSmem& S, CCache<V4>& cc_,
-                                           bool fits) {
+template <bool V4, class D>
+__device__ __forceinline__ void sp_project(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                           CCache<V4, D>& cc_) {
     typedef typename VecT<V4>::T VT;
-    constexpr int VW = V4 ? 4 : 1;
-    const int r = a.r, mv = a.m / VW;
+    typedef CCache<V4, D> CC_;
+    const int mv = Dm.m / CC_::VW;
     const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
     const VT* Pv = reinterpret_cast<const VT*>(S.sP);
-    for (int r0 = 0; r0 < r; r0 += RAE_NG * RAE_CRA) {
-        float s1[RAE_CRA], s2[RAE_CRA];
+    for (int r0 = 0; r0 < Dm.r; r0 += RAE_NG * CC_::RA) {
+        float s1[CC_::RA], s2[CC_::RA];
 #pragma unroll
-        for (int ra = 0; ra < RAE_CRA; ++ra) s1[ra] = s2[ra] = 0.f;
-        for (int c0 = 0; c0 < mv; c0 += 16 * RAE_CCC) {
-            if (!fits) cc_.load(a.C1, a.C2, r, mv, r0, c0);
+        for (int ra = 0; ra < CC_::RA; ++ra) s1[ra] = s2[ra] = 0.f;
+        for (int c0 = 0; c0 < mv; c0 += 16 * CC_::CC) {
+            if (!CC_::FITS) cc_.load(a, Dm, r0, c0);
 #pragma unroll
-            for (int cc = 0; cc < RAE_CCC; ++cc) {
-                const int c = c0 + q + 16 * cc;
-                if (c < mv) {
-                    const VT p = Pv[c];
+            for (int cc = 0; cc < CC_::CC; ++cc) {
+                const VT p = Pv[c0 + q + 16 * cc];          // zero beyond m (padded)
 #pragma unroll
-                    for (int ra = 0; ra < RAE_CRA; ++ra) {
-                        s1[ra] += vdot(cc_.c1[ra][cc], p);
-                        s2[ra] += vdot(cc_.c2[ra][cc], p);
-                    }
+                for (int ra = 0; ra < CC_::RA; ++ra) {
+                    s1[ra] += vdot(cc_.c1[ra][cc], p);
+                    s2[ra] += vdot(cc_.c2[ra][cc], p);
                 }
             }
         }
 #pragma unroll
-        for (int ra = 0; ra < RAE_CRA; ++ra) {
+        for (int ra = 0; ra < CC_::RA; ++ra) {
             const float t1 = group16_sum(s1[ra]);
             const float t2 = group16_sum(s2[ra]);
             const int i = r0 + gid + RAE_NG * ra;
-            if (q == 0 && i < r) {
+            if (q == 0 && i < Dm.r) {
                 S.swC1[i] = t1;
                 S.swC2[i] = t2;
             }
@@ -266,77 +225,194 @@ __device__ __forceinline__ void sp_project(const StepArgs& a, ExampleSmem& S, CC
     }
 }
 
-// dP = C1^T.dw1 + C2^T.dw2 (+ S.sdP already holding other dP terms) + entropy term,
-// then dS = softmax-backward; result in S.sdP.  has_c: C1/C2 terms present.
-template <bool V4>
-__device__ __forceinline__ void sp_project_back_and_softmax(const StepArgs& a, ExampleSmem& S,
-                                                            CCache<V4>& cc_, bool fits,
-                                                            bool has_c) {
+// dP += C1^T.dw1 + C2^T.dw2 into S.sdP (which holds any other dP terms)
+template <bool V4, class D>
+__device__ __forceinline__ void sp_project_back(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                                CCache<V4, D>& cc_) {
     typedef typename VecT<V4>::T VT;
-    constexpr int VW = V4 ? 4 : 1;
-    const int m = a.m, r = a.r, m4 = align4(m), mv = m / VW;
+    typedef CCache<V4, D> CC_;
+    constexpr int VW = CC_::VW;
+    const int mp = pad_m(Dm.m), mv = Dm.m / VW;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
-    if (has_c) {
-        for (int c0 = 0; c0 < mv; c0 += 16 * RAE_CCC) {
-            VT acc[RAE_CCC];
+    for (int c0 = 0; c0 < mv; c0 += 16 * CC_::CC) {
+        VT acc[CC_::CC];
 #pragma unroll
-            for (int cc = 0; cc < RAE_CCC; ++cc) vzero(acc[cc]);
-            for (int r0 = 0; r0 < r; r0 += RAE_NG * RAE_CRA) {
-                if (!fits) cc_.load(a.C1, a.C2, r, mv, r0, c0);
+        for (int cc = 0; cc < CC_::CC; ++cc) vzero(acc[cc]);
+        for (int r0 = 0; r0 < Dm.r; r0 += RAE_NG * CC_::RA) {
+            if (!CC_::FITS) cc_.load(a, Dm, r0, c0);
 #pragma unroll
-                for (int ra = 0; ra < RAE_CRA; ++ra) {
-                    const int i = r0 + gid + RAE_NG * ra;
-                    const float d1 = i < r ? S.sdw1[i] : 0.f;
-                    const float d2 = i < r ? S.sdw2[i] : 0.f;
+            for (int ra = 0; ra < CC_::RA; ++ra) {
+                const int i = r0 + gid + RAE_NG * ra;
+                const float d1 = i < Dm.r ? S.sdw1[i] : 0.f;
+                const float d2 = i < Dm.r ? S.sdw2[i] : 0.f;
 #pragma unroll
-                    for (int cc = 0; cc < RAE_CCC; ++cc) {
-                        vfma(acc[cc], d1, cc_.c1[ra][cc]);
-                        vfma(acc[cc], d2, cc_.c2[ra][cc]);
-                    }
+                for (int cc = 0; cc < CC_::CC; ++cc) {
+                    vfma(acc[cc], d1, cc_.c1[ra][cc]);
+                    vfma(acc[cc], d2, cc_.c2[ra][cc]);
                 }
             }
-            // reduce over the 4 lane groups of the wave, then waves through LDS
-#pragma unroll
-            for (int cc = 0; cc < RAE_CCC; ++cc) {
-                float* v = reinterpret_cast<float*>(&acc[cc]);
-#pragma unroll
-                for (int e = 0; e < VW; ++e) {
-                    v[e] += __shfl_xor(v[e], 16, 64);
-                    v[e] += __shfl_xor(v[e], 32, 64);
-                }
-                const int c = c0 + q + 16 * cc;
-                if (lane < 16 && c < mv)
-                    reinterpret_cast<VT*>(S.spart + w * m4)[c] = acc[cc];
-            }
-            __syncthreads();
-            for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-                const int cv = k / VW;
-                if (cv >= c0 && cv < c0 + 16 * RAE_CCC) {
-                    float dp = 0.f;
-#pragma unroll
-                    for (int ww = 0; ww < RAE_FNW; ++ww) dp += S.spart[ww * m4 + k];
-                    S.sdP[k] += dp;
-                }
-            }
-            __syncthreads();
         }
+        // reduce over the 4 lane groups of the wave (permlane swaps), then waves via LDS
+#pragma unroll
+        for (int cc = 0; cc < CC_::CC; ++cc) {
+            float* v = reinterpret_cast<float*>(&acc[cc]);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) {
+                v[e] += __uint_as_float(xor16_u32(__float_as_uint(v[e])));
+                v[e] += __uint_as_float(xor32_u32(__float_as_uint(v[e])));
+            }
+            if (lane < 16) reinterpret_cast<VT*>(S.spart + w * mp)[c0 + q + 16 * cc] = acc[cc];
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < Dm.m; k += RAE_FBT) {
+            const int cv = k / VW;
+            if (cv >= c0 && cv < c0 + 16 * CC_::CC) {
+                float dp = 0.f;
+#pragma unroll
+                for (int ww = 0; ww < RAE_FNW; ++ww) dp += S.spart[ww * mp + k];
+                S.sdP[k] += dp;
+            }
+        }
+        __syncthreads();
     }
+}
+
+// S = X.W + Wb spread over all threads (slot = feature lane group), then, in wave 0 (no
+// barriers) for m <= 512: softmax, log-softmax, entropy.  Issues the A-row LDS-DMA and the
+// decoder register cache behind the W-row loads.  Leaves H (alpha-scaled) in S.sred[40].
+template <bool V4, bool V4R, bool LOADC, class D, class Cache>
+__device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                                int NR, int skip_e2, Cache& cc_) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int m = Dm.m, mv = m / VW, mp = pad_m(m);
+    const int p0 = S.sint[0], p1 = S.sint[1];
+    const int nslot = RAE_FBT / mv > 0 ? RAE_FBT / mv : 1;
+    const int slot = threadIdx.x / mv, c = threadIdx.x - slot * mv;
+    const VT* Wv = reinterpret_cast<const VT*>(a.W);
+    VT acc;
+    vzero(acc);
+    bool issued = false;
+    for (int pc = p0; pc < p1; pc += RAE_FBT) {
+        const int nf = min(RAE_FBT, p1 - pc);
+        if (threadIdx.x < nf) {
+            S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
+            S.sfval[threadIdx.x] = a.values ? a.values[pc + threadIdx.x] : 1.f;
+        }
+        __syncthreads();
+        if (!issued) gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
+        if (slot < nslot) {
+            for (int cc = c; cc < mv; cc += RAE_FBT)          // mv > RAE_FBT only for huge m
+                for (int f = slot; f < nf; f += nslot)
+                    vfma(acc, S.sfval[f], Wv[(int64_t)S.sfidx[f] * mv + cc]);
+        }
+        if (LOADC && !issued) cc_.load(a, Dm, 0, 0);         // behind the W-row loads
+        issued = true;
+        __syncthreads();
+    }
+    if (!issued) {
+        gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
+        if (LOADC) cc_.load(a, Dm, 0, 0);
+    }
+    VT* part = reinterpret_cast<VT*>(S.spart);
+    if (slot < nslot && mv <= RAE_FBT) part[slot * mv + c] = acc;
+    __syncthreads();
+    float* sS = S.sdP;
+    for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
+        float v = 0.f;
+        if (k < m) {
+            for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
+            v += a.Wb[k];
+        }
+        sS[k] = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    if (m <= 8 * RAE_WAVE) {
+        if (threadIdx.x < RAE_WAVE) {                      // wave 0: no block barriers
+            float mx = -INFINITY;
+            for (int k = lane; k < m; k += RAE_WAVE) mx = fmaxf(mx, sS[k]);
+            mx = wave_max(mx);
+            float se = 0.f;
+            for (int k = lane; k < m; k += RAE_WAVE) se += expf(sS[k] - mx);
+            se = wave_sum(se);
+            const float lse = logf(se);
+            float hp = 0.f;
+            for (int k = lane; k < mp; k += RAE_WAVE) {
+                float lp = 0.f, p = 0.f;
+                if (k < m) {
+                    lp = (sS[k] - mx) - lse;
+                    p = expf(sS[k] - mx) / se;
+                }
+                S.slogP[k] = lp;
+                S.sP[k] = p;
+                hp += p * lp;
+            }
+            hp = wave_sum(hp);
+            if (lane == 0) S.sred[40] = -a.alpha * hp;
+        }
+    } else {
+        float mx = -INFINITY;
+        for (int k = threadIdx.x; k < m; k += RAE_FBT) mx = fmaxf(mx, sS[k]);
+        mx = block_max<RAE_FBT>(mx, S.sred);
+        float se = 0.f;
+        for (int k = threadIdx.x; k < m; k += RAE_FBT) se += expf(sS[k] - mx);
+        se = block_sum<RAE_FBT>(se, S.sred + 8);
+        const float lse = logf(se);
+        float hp = 0.f;
+        for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
+            float lp = 0.f, p = 0.f;
+            if (k < m) {
+                lp = (sS[k] - mx) - lse;
+                p = expf(sS[k] - mx) / se;
+            }
+            S.slogP[k] = lp;
+            S.sP[k] = p;
+            hp += p * lp;
+        }
+        hp = block_sum<RAE_FBT>(hp, S.sred + 16);
+        if (threadIdx.x == 0) S.sred[40] = -a.alpha * hp;
+    }
+    __syncthreads();
+}
+
+// entropy term + softmax backward: dS_k = P_k (dP_k - sum_j P_j dP_j), dP incl. the
+// entropy's (2 alpha / D)(log P_k + 1).  Wave 0 for m <= 512.
+template <class D>
+__device__ __forceinline__ void softmax_backward(const StepArgs& a, const D& Dm, ExampleSmem& S) {
+    const int m = Dm.m;
     const float ce = 2.f * a.alpha * a.invD;   // d cost / dH_b = -2/D ; dH/dP = -alpha(logP+1)
-    float sd = 0.f;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-        const float dp = S.sdP[k] + ce * (S.slogP[k] + 1.f);
-        S.sdP[k] = dp;
-        sd += S.sP[k] * dp;
+    const int lane = threadIdx.x & 63;
+    if (m <= 8 * RAE_WAVE) {
+        if (threadIdx.x < RAE_WAVE) {
+            float sd = 0.f;
+            for (int k = lane; k < m; k += RAE_WAVE) {
+                const float dp = S.sdP[k] + ce * (S.slogP[k] + 1.f);
+                S.sdP[k] = dp;
+                sd += S.sP[k] * dp;
+            }
+            sd = wave_sum(sd);
+            for (int k = lane; k < m; k += RAE_WAVE) S.sdP[k] = S.sP[k] * (S.sdP[k] - sd);
+        }
+    } else {
+        float sd = 0.f;
+        for (int k = threadIdx.x; k < m; k += RAE_FBT) {
+            const float dp = S.sdP[k] + ce * (S.slogP[k] + 1.f);
+            S.sdP[k] = dp;
+            sd += S.sP[k] * dp;
+        }
+        sd = block_sum<RAE_FBT>(sd, S.sred + 24);
+        for (int k = threadIdx.x; k < m; k += RAE_FBT) S.sdP[k] = S.sP[k] * (S.sdP[k] - sd);
     }
-    sd = block_sum<RAE_FBT>(sd, S.sred + 24);
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) S.sdP[k] = S.sP[k] * (S.sdP[k] - sd);
     __syncthreads();
 }
 
 // write the common part of the exchange record
-__device__ __forceinline__ void write_record(const StepArgs& a, ExampleSmem& S, float* rec) {
-    const int m = a.m, r = a.r, NJ = 2 + 2 * a.s;
+template <class D>
+__device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                             float* rec) {
+    const int m = Dm.m, r = Dm.r, NJ = 2 + 2 * Dm.s;
     for (int k = threadIdx.x; k < m; k += RAE_FBT) {
         rec[a.lay.oP + k] = S.sP[k];
         rec[a.lay.odS + k] = S.sdP[k];
@@ -351,54 +427,105 @@ __device__ __forceinline__ void write_record(const StepArgs& a, ExampleSmem& S, 
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
 }
 
+// v1[i] = c_a * row0[i] + sum_t coef1_t * rowsA_t[i],  v2 likewise (sums in t order):
+// thread owns (vector column, row group); groups combined in LDS in fixed order.
+template <bool V4, class D>
+__device__ __forceinline__ void sp_weighted_rows(const D& Dm, ExampleSmem& S) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int s = Dm.s, r4 = align4(Dm.r), rv = Dm.r / VW;
+    const int ngrp = RAE_FBT / rv > 8 ? 8 : (RAE_FBT / rv > 0 ? RAE_FBT / rv : 1);
+    const int grp = threadIdx.x / rv, c = threadIdx.x - grp * rv;
+    VT* part = reinterpret_cast<VT*>(S.spart);                 // [2][ngrp][rv]
+    if (grp < ngrp && rv <= RAE_FBT) {
+        const VT* R = reinterpret_cast<const VT*>(S.srows);
+        const int r4v = r4 / VW;
+        VT v1, v2;
+        vzero(v1);
+        vzero(v2);
+        if (grp == 0) {
+            const VT a1 = R[c];
+            vfma(v1, S.scoef[0], a1);
+            vfma(v2, S.scoef[1], a1);
+        }
+        for (int t = grp; t < s; t += ngrp) {
+            vfma(v1, S.scoef[3 * (2 + t)], R[(1 + t) * r4v + c]);
+            vfma(v2, S.scoef[3 * (2 + s + t) + 1], R[(1 + s + t) * r4v + c]);
+        }
+        part[grp * rv + c] = v1;
+        part[(ngrp + grp) * rv + c] = v2;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < Dm.r; i += RAE_FBT) {
+        float v1 = 0.f, v2 = 0.f;
+        for (int gg = 0; gg < ngrp; ++gg) {
+            v1 += S.spart[gg * Dm.r + i];
+            v2 += S.spart[(ngrp + gg) * Dm.r + i];
+        }
+        S.sdw1[i] = v1;
+        S.sdw2[i] = v2;
+    }
+}
+
 // ---- the SP example path ---------------------------------------------------------------
-template <bool V4M, bool V4R>
+template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
-    const int m = a.m, r = a.r, s = a.s, NR = 1 + 2 * s;
-    const int r4 = align4(r);
+    const D Dm(a);
+    const int m = Dm.m, r = Dm.r, s = Dm.s, NR = 1 + 2 * s;
+    const int r4 = align4(r), mp = pad_m(m);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int VWM = V4M ? 4 : 1;
+    constexpr int VW = V4 ? 4 : 1;
+    typedef typename VecT<V4>::T VT;
     ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
 
-    // round trip 1: ids + feature range; C1/C2 register cache (independent of everything)
-    CCache<V4M> cc_;
-    const bool fits = ccache_fits(r, m / VWM);
-    if (fits) cc_.load(a.C1, a.C2, r, m / VWM, 0, 0);
-    load_ids(a, ex, col, S);
+    RAE_STAMP(a, 0);
+#ifdef RAE_STAMPS
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
+#endif
+    load_ids(a, Dm, ex, col, S);
     __syncthreads();
-    // round trip 2: Ab values, A-row gather (prefetched into registers), features, W rows
+    RAE_STAMP(a, 1);
     const int NJ = 2 + 2 * s;
-    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) S.sAbv[j] = a.Ab[S.sids[j]];
-    const float H = encoder_forward<V4M, V4R>(a, S, NR, 1);
+    if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
+    CCache<V4, D> cc_;
+    encoder_forward<V4, V4, CCache<V4, D>::FITS>(a, Dm, S, NR, 1, cc_);
+    const float H = S.sred[40];
+    RAE_STAMP(a, 2);
+    sp_project<V4>(a, Dm, S, cc_);
     __syncthreads();
-    sp_project<V4M>(a, S, cc_, fits);
-    __syncthreads();
+    RAE_STAMP(a, 3);
 
-    // dot products: row rho on wave rho % NW
-    for (int rho = w; rho < NR; rho += RAE_FNW) {
-        const float* row = S.srows + rho * r4;
-        float d1 = 0.f, d2 = 0.f;
-        const bool isn2 = rho > s;                // rows 1..s: neg1, s+1..2s: neg2
-        const float* wv = isn2 ? S.swC2 : S.swC1;
-        for (int i = lane; i < r; i += RAE_WAVE) {
-            d1 += row[i] * wv[i];
-            if (rho == 0) d2 += row[i] * S.swC2[i];
-        }
-        d1 = wave_sum(d1);
-        if (rho == 0) d2 = wave_sum(d2);
-        if (lane == 0) {
-            if (rho == 0) {
-                S.sdots[0] = d1;     // left  = <wC1, A[e1]>
-                S.sdots[1] = d2;     // right = <wC2, A[e1]>
-            } else {
-                S.sdots[rho + 1] = d1;   // record j = rho + 1
+    // dot products: row rho on wave rho % NW; lanes over vector columns
+    {
+        const int rv = r / VW, r4v = r4 / VW;
+        const VT* Rv = reinterpret_cast<const VT*>(S.srows);
+        const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
+        const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
+        for (int rho = w; rho < NR; rho += RAE_FNW) {
+            const VT* wv = rho > s ? W2 : W1;      // rows 1..s: neg1, s+1..2s: neg2
+            float d1 = 0.f, d2 = 0.f;
+            for (int c = lane; c < rv; c += RAE_WAVE) {
+                const VT x = Rv[rho * r4v + c];
+                d1 += vdot(x, wv[c]);
+                if (rho == 0) d2 += vdot(x, W2[c]);
+            }
+            d1 = wave_sum(d1);
+            if (rho == 0) d2 = wave_sum(d2);
+            if (lane == 0) {
+                if (rho == 0) {
+                    S.sdots[0] = d1;     // left  = <wC1, A[e1]>
+                    S.sdots[1] = d2;     // right = <wC2, A[e1]>
+                } else {
+                    S.sdots[rho + 1] = d1;   // record j = rho + 1
+                }
             }
         }
     }
     __syncthreads();
+    RAE_STAMP(a, 4);
 
     // scores, loss, coefficients (wave 0)
     if (w == 0) {
@@ -435,20 +562,18 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     __syncthreads();
 
     // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
-    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        const float a1 = S.srows[i];
-        float v1 = S.scoef[0] * a1, v2 = S.scoef[1] * a1;
-        for (int t = 0; t < s; ++t) {
-            v1 += S.scoef[3 * (2 + t)] * S.srows[(1 + t) * r4 + i];
-            v2 += S.scoef[3 * (2 + s + t) + 1] * S.srows[(1 + s + t) * r4 + i];
-        }
-        S.sdw1[i] = v1;
-        S.sdw2[i] = v2;
-    }
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) S.sdP[k] = 0.f;
+    sp_weighted_rows<V4>(Dm, S);
+    for (int k = threadIdx.x; k < mp; k += RAE_FBT) S.sdP[k] = 0.f;
     __syncthreads();
-    sp_project_back_and_softmax<V4M>(a, S, cc_, fits, true);
-    write_record(a, S, a.ex + (int64_t)bg * a.lay.rec);
+    RAE_STAMP(a, 5);
+    sp_project_back<V4>(a, Dm, S, cc_);
+    softmax_backward(a, Dm, S);
+    RAE_STAMP(a, 6);
+    write_record(a, Dm, S, a.ex + (int64_t)bg * a.lay.rec);
+    RAE_STAMP(a, 7);
+#ifdef RAE_STAMPS
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 }  // namespace rae

@@ -62,10 +62,11 @@ struct StepArgs {
     // exchange records
     float* ex;
     RecLayout lay;
-    // per-step row index of the global batch (hash partitions, row % H)
+    // row index of the global batches (rae_index.hpp), one slot per batch % index_window
     int HA, HW, RA, RW, posbits;
-    int32_t *hdrA, *srecA, *urowA, *ustartA;
-    int32_t *hdrW, *srecW, *urowW, *ustartW;
+    int64_t index_window;
+    int32_t *hdrA, *srecA, *urowA;      // urow*: interleaved (row, first position) pairs
+    int32_t *hdrW, *srecW, *urowW;
     // batch addressing, outputs, scratch
     const int64_t* cursor;
     int64_t step_offset;
@@ -76,6 +77,17 @@ struct StepArgs {
     int nregW;           // number of dense-W block partial slots
     float* base_cost;    // cost before the regulariser (reg_on only)
     int* err;            // device error word
+    unsigned long long* stamps;   // diagnostic build only (RAE_STAMPS): phase timestamps
 };
+
+#ifdef RAE_STAMPS
+#define RAE_STAMP(a, slot)                                                                  \
+    do {                                                                                    \
+        if ((a).stamps && threadIdx.x == 0)                                                 \
+            (a).stamps[(size_t)blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define RAE_STAMP(a, slot) do { } while (0)
+#endif
 
 }  // namespace rae

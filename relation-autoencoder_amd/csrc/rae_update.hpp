@@ -29,7 +29,7 @@ namespace rae {
 //   D[row][col]            col = lane&15, row = (lane>>4)*4 + reg
 // SP/hybrid C1, C2: coef(b, i) = dw1_b[i] / dw2_b[i]; Wb (ones): one row of ones times dS_b.
 typedef float rae_f4 __attribute__((ext_vector_type(4)));
-#define RAE_TU 8     // k-steps (x4 examples) whose operands are loaded before the MFMA chain
+#define RAE_TU 32    // k-steps (x4 examples) whose operands are loaded before the MFMA chain
 
 template <int OPT>
 __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw,
@@ -154,16 +154,16 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 // g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per record),
 // the record vectors RAE_UNR at a time with every load issued before the first FMA.
 template <int OPT, bool V4, int Q, bool XY>
-__device__ void task_entity_row(const StepArgs& a, int h, int u, int lane) {
+__device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, int C, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? 8 : 4;
     typedef typename VecT<V4>::T VT;
     const int r = a.r, nv = r / VW, NJ = 2 + 2 * a.s;
-    const int32_t* hdr = a.hdrA + 2 * h;
-    const int64_t base = (int64_t)h * a.RA;
-    const int e = a.urowA[base + u];
-    const int st = a.ustartA[base + u];
-    const int en = (u + 1 < hdr[1]) ? a.ustartA[base + u + 1] : hdr[0];
+    const int64_t base = slot * a.RA;
+    const int2 seg = reinterpret_cast<const int2*>(a.urowA + 2 * base)[u];
+    const int nxt = a.urowA[2 * base + 2 * (u + 1 < U ? u + 1 : u) + 1];
+    const int e = seg.x, st = seg.y;
+    const int en = (u + 1 < U) ? nxt : C;
     float* prow = a.A + (int64_t)e * r;
     float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
     RowVec<V4, Q> pv, av, g;
@@ -236,16 +236,17 @@ __device__ void task_entity_row(const StepArgs& a, int h, int u, int lane) {
 
 // ---- W rows: g(W[f]) = sum over the row's CSR records of x_bf * dS_b ----------------------
 template <int OPT, bool V4, int Q>
-__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int h, int u, int lane) {
+__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int u, int U,
+                                 int C, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? 8 : 4;
     typedef typename VecT<V4>::T VT;
     const int m = a.m, nv = m / VW;
-    const int32_t* hdr = a.hdrW + 2 * h;
-    const int64_t base = (int64_t)h * a.RW;
-    const int f = a.urowW[base + u];
-    const int st = a.ustartW[base + u];
-    const int en = (u + 1 < hdr[1]) ? a.ustartW[base + u + 1] : hdr[0];
+    const int64_t base = slot * a.RW;
+    const int2 seg = reinterpret_cast<const int2*>(a.urowW + 2 * base)[u];
+    const int nxt = a.urowW[2 * base + 2 * (u + 1 < U ? u + 1 : u) + 1];
+    const int f = seg.x, st = seg.y;
+    const int en = (u + 1 < U) ? nxt : C;
     const unsigned mask = (1u << a.posbits) - 1u;
     float* prow = a.W + (int64_t)f * m;
     float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;

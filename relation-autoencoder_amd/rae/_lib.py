@@ -23,7 +23,7 @@ EXPORTS = (
     "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version",
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
     "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
-    "rae_train_step", "rae_check", "rae_label",
+    "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
 )
 
 
@@ -36,6 +36,7 @@ class RaeConfig(C.Structure):
         ("learning_rate", C.c_float), ("alpha", C.c_float), ("lambda1", C.c_float),
         ("lambda2", C.c_float), ("ext_reg", C.c_int32), ("max_batch_nnz", C.c_int32),
         ("max_row_nnz", C.c_int32), ("neg_mode", C.c_int32), ("neg_stride", C.c_int64),
+        ("index_window", C.c_int64),
     ]
 
 
@@ -84,10 +85,13 @@ def load(path: str | None = None):
     lib.rae_step_update.argtypes = [_P, C.c_int64, _P]
     lib.rae_train_step.argtypes = [_P, C.c_int64, _P, _P, _P]
     lib.rae_check.argtypes = [_P]
+    lib.rae_build_index.argtypes = [_P, C.c_int64, C.c_int64, _P]
+    lib.rae_index_window.argtypes = [_P]
+    lib.rae_index_window.restype = C.c_int64
     lib.rae_label.argtypes = [_P, _P, _P, _P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, _P]
     for fn in ("rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
-               "rae_check", "rae_label"):
+               "rae_check", "rae_label", "rae_build_index"):
         getattr(lib, fn).restype = C.c_int
     if path is None:
         _lib = lib

@@ -46,7 +46,7 @@ class DeviceSplit:
 class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
-                 device=None):
+                 index_window=0, device=None):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -87,6 +87,7 @@ class TrainEngine:
         cfg.max_row_nnz = mrn
         cfg.neg_mode = _lib.RAE_NEG_PER_EPOCH
         cfg.neg_stride = self.N
+        cfg.index_window = int(index_window)
         self.cfg = cfg
         self.rec_floats = int(self.lib.rae_exchange_record_floats(C.byref(cfg)))
         self.exchange_buf = torch.zeros(int(self.lib.rae_exchange_floats(C.byref(cfg))),
@@ -116,6 +117,7 @@ class TrainEngine:
         _lib.check(self.lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(handle)),
                    "rae_plan_create")
         self.plan = handle
+        self.index_window = int(self.lib.rae_index_window(self.plan))
         self._graphs = {}
         self._epoch_mode = None
 
@@ -201,21 +203,27 @@ class TrainEngine:
 
     def run(self, first_batch: int, count: int, graph: bool = True):
         """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
-        negatives; costs land in self.costs[first_batch:first_batch+count]."""
+        negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
+        of each window of batches is built right before the window's steps."""
         self._ensure_epoch_mode()
-        st = self._stream()
-        _lib.check(self.lib.rae_set_cursor(self.plan, int(first_batch), st), "rae_set_cursor")
-        if not graph or self.graph_chunk <= 1:
-            self._steps_eager(count, st)
-            return
-        T = self.graph_chunk
-        full, rem = divmod(int(count), T)
-        if full:
-            g = self._graph(T)
-            for _ in range(full):
-                g.replay()
-        if rem:
-            self._steps_eager(rem, self._stream())
+        b, end = int(first_batch), int(first_batch) + int(count)
+        while b < end:
+            n = min(self.index_window, end - b)
+            st = self._stream()
+            _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
+            _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
+            if not graph or self.graph_chunk <= 1:
+                self._steps_eager(n, st)
+            else:
+                T = self.graph_chunk
+                full, rem = divmod(n, T)
+                if full:
+                    g = self._graph(T)
+                    for _ in range(full):
+                        g.replay()
+                if rem:
+                    self._steps_eager(rem, self._stream())
+            b += n
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):
