@@ -1,10 +1,11 @@
 // MI355X (gfx950) relation-autoencoder training path: kernels + C ABI (include/rae.h).
 //
 // Per training step (one func['train'] call of learning/OieInduction.py:189):
-//   k_forward  grid = HA + HW index workgroups + l example workgroups
-//              index WGs : per-step row index of the global batch (rae_index.hpp)
-//              example WG: encoder + decoder forward/backward of one example (rae_sp.hpp,
-//                          rae_bilinear.hpp) -> exchange record
+//   SP:        k_forward  one workgroup per example: encoder + decoder forward/backward
+//                         (rae_sp.hpp) -> exchange record
+//   bilinear:  k_bil_enc -> k_bil_m (MFMA) -> k_bil_dec -> k_bil_dp (MFMA) -> k_bil_fin
+//                         (rae_bilinear.hpp) -> exchange record
+//   (the per-batch row index is built ahead, a window of batches at a time: k_build_index)
 //   [caller all-gathers the exchange records across data-parallel ranks]
 //   k_update   one wavefront per distinct referenced row / dense decoder row / bias:
 //              deterministic gradient sums + AdaGrad/SGD in place (rae_update.hpp)
@@ -31,13 +32,44 @@ using namespace rae;
 // ======================================================================================
 // kernels
 // ======================================================================================
-template <int DEC, bool V4, class D>
+template <bool V4, class D>
 __global__ __launch_bounds__(RAE_FBT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = *a.cursor + a.step_offset;
-    if (DEC == RAE_DEC_SP) sp_example<V4, D>(a, g, blockIdx.x, smem);
-    else bilinear_example<V4>(a, g, blockIdx.x, smem, DEC == RAE_DEC_HYBRID);
+    sp_example<V4, D>(a, g, blockIdx.x, smem);
+}
+
+// ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
+template <bool V4>
+__global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bil_encode<V4>(a, *a.cursor + a.step_offset, blockIdx.x, smem);
+}
+__host__ __device__ inline int bil_m_tasks(int l, int r) {
+    return ((l + 15) / 16) * (int)(((int64_t)r * r + 63) / 64);
+}
+template <bool V4>
+__global__ __launch_bounds__(RAE_BT) void k_bil_m(StepArgs a) {
+    const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    if (t < bil_m_tasks(a.l, a.r)) bil_gemm_m<V4>(a, t, threadIdx.x & 63);
+}
+template <bool V4>
+__global__ __launch_bounds__(RAE_FBT) void k_bil_dec(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bil_decode<V4>(a, *a.cursor + a.step_offset, blockIdx.x, smem);
+}
+__host__ __device__ inline int bil_dp_tasks(int l, int m, int nib) {
+    return ((l + 15) / 16) * ((m + 15) / 16) * nib;
+}
+__global__ __launch_bounds__(RAE_BT) void k_bil_dp(StepArgs a) {
+    const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    if (t < bil_dp_tasks(a.l, a.m, a.nib)) bil_gemm_dp(a, t, threadIdx.x & 63);
+}
+__global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
+    __shared__ float sdp[1024];
+    __shared__ float red[2 * RAE_NWAVE];
+    bil_finish(a, blockIdx.x, sdp, red);
 }
 
 // shapes with compile-time specialisations of the forward kernel (BASELINE.json configs
@@ -57,7 +89,7 @@ __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
     return dec != RAE_DEC_RESCAL ? 2 * ((r + 15) / 16) * ((m + 15) / 16) : 0;
 }
 __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
-    return dec != RAE_DEC_SP ? ((r * r + 15) / 16) * ((m + 15) / 16) : 0;
+    return dec != RAE_DEC_SP ? (r * r + 15) / 16 : 0;    // 16 rows of R/C x all m each
 }
 
 #ifdef RAE_STAMPS
@@ -110,7 +142,7 @@ __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
         }
         tt -= nCt;
         if (BIL && tt < nRt) {
-            task_bilinear_tile<OPT>(a, (tt / mt) * 16, (tt % mt) * 16, nCt + tt, lane);
+            task_bilinear_rows<OPT>(a, tt, nCt + tt, lane);
             RAE_WAVE_END();
             continue;
         }
@@ -285,6 +317,7 @@ struct rae_plan {
     char* ws = nullptr;
     size_t smem_fwd = 0;
     size_t smem_idx = 0;
+    size_t smem_dec = 0;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
     int q = 1;
@@ -426,6 +459,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(8ull * W_ * a.RW);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
+    const bool bil = c.decoder != RAE_DEC_SP;
+    a.nib = bil ? (c.embed + RAE_IB - 1) / RAE_IB : 0;
+    const size_t o_mbuf = bil ? take(4ull * c.batch_size * c.embed * c.embed) : 0;
+    const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
     if (e != hipSuccess) {
         delete p;
@@ -446,6 +483,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
+    a.Mbuf = bil ? reinterpret_cast<float*>(p->ws + o_mbuf) : nullptr;
+    a.dPpart = bil ? reinterpret_cast<float*>(p->ws + o_dpp) : nullptr;
     a.err = p->d_err;
     a.cursor = p->d_cursor;
 
@@ -453,7 +492,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t smem_ex = 4ull * ex_floats;
     p->smem_idx = 8ull * RAE_KCAP + 4ull * (33 + L + 1);
     p->smem_fwd = smem_ex;
-    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024) {
+    p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
+    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024) {
         (void)hipFree(p->ws);
         delete p;
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
@@ -463,17 +503,20 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     int gu = ceil_div(tasks, RAE_NWAVE);
     p->grid_update = gu < 1 ? 1 : (gu > 8192 ? 8192 : gu);
     {
-        const void* fns[] = {(const void*)k_forward<RAE_DEC_SP, true, DimsC3>,
-                             (const void*)k_forward<RAE_DEC_SP, false, DimsC2>,
-                             (const void*)k_forward<RAE_DEC_SP, true, DynDims>,
-                             (const void*)k_forward<RAE_DEC_SP, false, DynDims>,
-                             (const void*)k_forward<RAE_DEC_RESCAL, true, DynDims>,
-                             (const void*)k_forward<RAE_DEC_RESCAL, false, DynDims>,
-                             (const void*)k_forward<RAE_DEC_HYBRID, true, DynDims>,
-                             (const void*)k_forward<RAE_DEC_HYBRID, false, DynDims>};
+        const void* fns[] = {(const void*)k_forward<true, DimsC3>,
+                             (const void*)k_forward<false, DimsC2>,
+                             (const void*)k_forward<true, DynDims>,
+                             (const void*)k_forward<false, DynDims>,
+                             (const void*)k_bil_enc<true>, (const void*)k_bil_enc<false>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p->smem_fwd);
+        if (bil) {
+            (void)hipFuncSetAttribute((const void*)k_bil_dec<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
+            (void)hipFuncSetAttribute((const void*)k_bil_dec<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
+        }
         (void)hipFuncSetAttribute((const void*)k_build_index,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
     }
@@ -513,25 +556,30 @@ extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t strea
     return RAE_OK;
 }
 
-template <int DEC>
-static void launch_fwd_dec(rae_plan* p, const StepArgs& a, hipStream_t st) {
+static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 gr(p->grid_fwd), bt(RAE_FBT);
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;
     const bool c2 = a.m == 30 && a.r == 100 && a.s == 10;
-    if constexpr (DEC == RAE_DEC_SP) {
-        if (c3 && p->v4) {
-            hipLaunchKernelGGL((k_forward<DEC, true, DimsC3>), gr, bt, p->smem_fwd, st, a);
-            return;
-        }
-        if (c2 && !p->v4) {
-            hipLaunchKernelGGL((k_forward<DEC, false, DimsC2>), gr, bt, p->smem_fwd, st, a);
-            return;
-        }
-    }
-    if (p->v4)
-        hipLaunchKernelGGL((k_forward<DEC, true, DynDims>), gr, bt, p->smem_fwd, st, a);
+    if (c3 && p->v4)
+        hipLaunchKernelGGL((k_forward<true, DimsC3>), gr, bt, p->smem_fwd, st, a);
+    else if (c2 && !p->v4)
+        hipLaunchKernelGGL((k_forward<false, DimsC2>), gr, bt, p->smem_fwd, st, a);
+    else if (p->v4)
+        hipLaunchKernelGGL((k_forward<true, DynDims>), gr, bt, p->smem_fwd, st, a);
     else
-        hipLaunchKernelGGL((k_forward<DEC, false, DynDims>), gr, bt, p->smem_fwd, st, a);
+        hipLaunchKernelGGL((k_forward<false, DynDims>), gr, bt, p->smem_fwd, st, a);
+}
+
+template <bool V4>
+static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
+    const dim3 ge(p->grid_fwd);
+    hipLaunchKernelGGL((k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
+    const int gm = ceil_div(bil_m_tasks(a.l, a.r), RAE_NWAVE);
+    hipLaunchKernelGGL((k_bil_m<V4>), dim3(gm), dim3(RAE_BT), 0, st, a);
+    hipLaunchKernelGGL((k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
+    const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
+    hipLaunchKernelGGL(k_bil_dp, dim3(gd), dim3(RAE_BT), 0, st, a);
+    hipLaunchKernelGGL(k_bil_fin, ge, dim3(RAE_BT), 0, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
@@ -540,11 +588,9 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     a.cursor = cursor;
     a.step_offset = off;
     a.stamps = p->stamps_fwd;
-    switch (a.dec) {
-        case RAE_DEC_SP: launch_fwd_dec<RAE_DEC_SP>(p, a, st); break;
-        case RAE_DEC_RESCAL: launch_fwd_dec<RAE_DEC_RESCAL>(p, a, st); break;
-        default: launch_fwd_dec<RAE_DEC_HYBRID>(p, a, st); break;
-    }
+    if (a.dec == RAE_DEC_SP) launch_fwd_sp(p, a, st);
+    else if (p->v4) launch_fwd_bil<true>(p, a, st);
+    else launch_fwd_bil<false>(p, a, st);
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }

@@ -48,7 +48,7 @@ template <class D> struct DimT { static constexpr int m = 0, r = 0; };
 template <int M, int R, int S> struct DimT<FixDims<M, R, S>> { static constexpr int m = M, r = R; };
 
 struct ExampleSmem {
-    float *sP, *slogP, *sdP, *swC1, *swC2, *sdw1, *sdw2, *srows, *sdots, *sAbv, *scoef,
+    float *sP, *sZ, *sdP, *swC1, *swC2, *sdw1, *sdw2, *srows, *sdots, *sAbv, *scoef,
         *sred, *spart, *sfval, *sX, *sY, *sM;
     int *sfidx, *sids, *sint;
 };
@@ -76,7 +76,7 @@ __device__ inline ExampleSmem carve_example_smem(char* smem, int dec, int m, int
     if (16 * r4 > partf) partf = 16 * r4;
     float* p = reinterpret_cast<float*>(smem);
     S.sP = p; p += mp;
-    S.slogP = p; p += mp;
+    S.sZ = p; p += mp;            // shifted scores z = S - max S (encoder_forward)
     S.sdP = p; p += mp;
     S.swC1 = p; p += r4;
     S.swC2 = p; p += r4;
@@ -279,8 +279,9 @@ __device__ __forceinline__ void sp_project_back(const StepArgs& a, const D& Dm, 
 }
 
 // S = X.W + Wb spread over all threads (slot = feature lane group), then, in wave 0 (no
-// barriers) for m <= 512: softmax, log-softmax, entropy.  Issues the A-row LDS-DMA and the
-// decoder register cache behind the W-row loads.  Leaves H (alpha-scaled) in S.sred[40].
+// barriers) for m <= 512: softmax, entropy.  Issues the A-row LDS-DMA and the decoder
+// register cache behind the W-row loads.  Leaves H (alpha-scaled) in S.sred[40] and the
+// shifted scores z = S - max(S) in S.sZ (log P = z - lse; see softmax_backward).
 template <bool V4, bool V4R, bool LOADC, class D, class Cache>
 __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, ExampleSmem& S,
                                                 int NR, int skip_e2, Cache& cc_) {
@@ -340,14 +341,14 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
             const float lse = logf(se);
             float hp = 0.f;
             for (int k = lane; k < mp; k += RAE_WAVE) {
-                float lp = 0.f, p = 0.f;
+                float z = 0.f, p = 0.f;
                 if (k < m) {
-                    lp = (sS[k] - mx) - lse;
-                    p = expf(sS[k] - mx) / se;
+                    z = sS[k] - mx;
+                    p = expf(z) / se;
                 }
-                S.slogP[k] = lp;
+                S.sZ[k] = z;
                 S.sP[k] = p;
-                hp += p * lp;
+                hp += p * (z - lse);
             }
             hp = wave_sum(hp);
             if (lane == 0) S.sred[40] = -a.alpha * hp;
@@ -362,14 +363,14 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         const float lse = logf(se);
         float hp = 0.f;
         for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
-            float lp = 0.f, p = 0.f;
+            float z = 0.f, p = 0.f;
             if (k < m) {
-                lp = (sS[k] - mx) - lse;
-                p = expf(sS[k] - mx) / se;
+                z = sS[k] - mx;
+                p = expf(z) / se;
             }
-            S.slogP[k] = lp;
+            S.sZ[k] = z;
             S.sP[k] = p;
-            hp += p * lp;
+            hp += p * (z - lse);
         }
         hp = block_sum<RAE_FBT>(hp, S.sred + 16);
         if (threadIdx.x == 0) S.sred[40] = -a.alpha * hp;
@@ -377,33 +378,40 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     __syncthreads();
 }
 
-// entropy term + softmax backward: dS_k = P_k (dP_k - sum_j P_j dP_j), dP incl. the
-// entropy's (2 alpha / D)(log P_k + 1).  Wave 0 for m <= 512.
+// entropy term + softmax backward.  With d = the decoder's dCost/dP and the entropy's
+// dCost/dP_k = ce (log P_k + 1), ce = 2 alpha / D (cost has -2H/D, dH/dP = -alpha(logP+1)):
+//   dS_k = P_k (dP_k - sum_j P_j dP_j) = P_k ((d_k - sum_j P_j d_j) + ce (z_k - sum_j P_j z_j))
+// with z = S - max S (log P - sum P log P is shift invariant).  The centred form avoids the
+// cancellation of the large constant log P + 1 against its mean, which in fp32 costs ~1e-7
+// relative to log m -- more than the whole signal when P is near uniform.  Wave 0 for
+// m <= 512.
 template <class D>
 __device__ __forceinline__ void softmax_backward(const StepArgs& a, const D& Dm, ExampleSmem& S) {
     const int m = Dm.m;
-    const float ce = 2.f * a.alpha * a.invD;   // d cost / dH_b = -2/D ; dH/dP = -alpha(logP+1)
+    const float ce = 2.f * a.alpha * a.invD;
     const int lane = threadIdx.x & 63;
     if (m <= 8 * RAE_WAVE) {
         if (threadIdx.x < RAE_WAVE) {
-            float sd = 0.f;
+            float sd = 0.f, sz = 0.f;
             for (int k = lane; k < m; k += RAE_WAVE) {
-                const float dp = S.sdP[k] + ce * (S.slogP[k] + 1.f);
-                S.sdP[k] = dp;
-                sd += S.sP[k] * dp;
+                sd += S.sP[k] * S.sdP[k];
+                sz += S.sP[k] * S.sZ[k];
             }
             sd = wave_sum(sd);
-            for (int k = lane; k < m; k += RAE_WAVE) S.sdP[k] = S.sP[k] * (S.sdP[k] - sd);
+            sz = wave_sum(sz);
+            for (int k = lane; k < m; k += RAE_WAVE)
+                S.sdP[k] = S.sP[k] * ((S.sdP[k] - sd) + ce * (S.sZ[k] - sz));
         }
     } else {
-        float sd = 0.f;
+        float sd = 0.f, sz = 0.f;
         for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-            const float dp = S.sdP[k] + ce * (S.slogP[k] + 1.f);
-            S.sdP[k] = dp;
-            sd += S.sP[k] * dp;
+            sd += S.sP[k] * S.sdP[k];
+            sz += S.sP[k] * S.sZ[k];
         }
         sd = block_sum<RAE_FBT>(sd, S.sred + 24);
-        for (int k = threadIdx.x; k < m; k += RAE_FBT) S.sdP[k] = S.sP[k] * (S.sdP[k] - sd);
+        sz = block_sum<RAE_FBT>(sz, S.sred + 48);
+        for (int k = threadIdx.x; k < m; k += RAE_FBT)
+            S.sdP[k] = S.sP[k] * ((S.sdP[k] - sd) + ce * (S.sZ[k] - sz));
     }
     __syncthreads();
 }

@@ -4,15 +4,21 @@
 
 namespace rae {
 
-// Per-example record in the exchange buffer (floats).  Layout is decoder-independent:
-//   P (m) | dS (m) | V1 (r) | V2 (r) | dw1 (r) | dw2 (r) | coef (3*NJ) | loss (1) | pad
-// SP       : V1 = wC1 = C1.P, V2 = wC2, dw1/dw2 = dCost/dwC1, dCost/dwC2,
-//            coef[j] = (alpha_j, beta_j, gamma_j): record j's A-row gradient is
-//            alpha_j*V1 + beta_j*V2 and its Ab gradient gamma_j.
-// RESCAL / hybrid use the same slots with their own basis vectors (rae_bilinear.hpp).
+// Per-example record in the exchange buffer (floats).
+//   P (m) | dS (m) | V1 (r) | V2 (r) | dw1 (r) | dw2 (r) |
+//   [bilinear: G1 (r) | G2 (r) | X (r) | Y (r) | A1 (r) | A2 (r) | z = S - max S (m)] |
+//   coef (3*NJ) | loss (1) | pad
+// coef[j] = (alpha_j, beta_j, gamma_j) for record j (0: e1, 1: e2, 2..: neg1[t], neg2[t]):
+// record j's A-row gradient is alpha_j*V1 + beta_j*V2 (+ G1 for j = 0, G2 for j = 1 on the
+// bilinear decoders) and its Ab gradient gamma_j.
+// SP       : V1 = wC1 = C1.P, V2 = wC2, dw1/dw2 = dCost/dwC1, dCost/dwC2.
+// bilinear : V1 = M a2 (+ wC1), V2 = M^T a1 (+ wC2) with M = sum_k P_k R[:,:,k];
+//            G1/G2 = the full A-row gradients of e1/e2; X, Y, A1, A2 the rank-2 factors of
+//            dCost/dM = X A2^T + A1 Y^T (A1/A2 = copies of A[e1], A[e2] taken before the
+//            update kernel changes A); dw1/dw2 as SP for the hybrid.
 struct RecLayout {
     int oP, odS, oV1, oV2, odw1, odw2, ocoef, oloss, rec;
-    int oX, oY;   // bilinear factor vectors x_b, y_b (RESCAL/hybrid) ; 0 for SP
+    int oG1, oG2, oX, oY, oA1, oA2, oZ;   // bilinear decoders only (0 for SP)
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
@@ -28,9 +34,14 @@ __host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s) {
     L.odw1 = L.oV2 + r4;
     L.odw2 = L.odw1 + r4;
     int o = L.odw2 + r4;
-    if (dec != 0) {          // bilinear factors + the two extra A-row basis vectors
-        L.oX = o; o += r4;    // x_b  (left factor of dM_b)
-        L.oY = o; o += r4;    // y_b  (right factor with a1)
+    if (dec != 0) {
+        L.oG1 = o; o += r4;
+        L.oG2 = o; o += r4;
+        L.oX = o; o += r4;
+        L.oY = o; o += r4;
+        L.oA1 = o; o += r4;
+        L.oA2 = o; o += r4;
+        L.oZ = o; o += m4;
     }
     L.ocoef = o;
     o += align4(3 * NJ);
@@ -72,6 +83,9 @@ struct StepArgs {
     int64_t step_offset;
     float* costs;
     float* gWs;          // dense W gradient scratch (reg_on only)
+    float* Mbuf;         // bilinear: M_b = sum_k P_bk R[:,:,k] of this rank's examples (l, r*r)
+    float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
+    int nib;             // bilinear: number of i-blocks of the dP contraction
     double* regpart;     // [nreg][2] L1/L2 partials of regularised rows
     int nregC;           // number of decoder-row partial slots
     int nregW;           // number of dense-W block partial slots

@@ -150,7 +150,7 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 
 // ---- A / Ab rows -------------------------------------------------------------------------
 // g(A[e]) = sum over the row's records (in sorted order) of
-//   alpha_j * V1_b + beta_j * V2_b (+ X_b for j = 0 / Y_b for j = 1 when XY)
+//   alpha_j * V1_b + beta_j * V2_b (+ G1_b for j = 0 / G2_b for j = 1 when XY: bilinear)
 // g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per record),
 // the record vectors RAE_UNR at a time with every load issued before the first FMA.
 template <int OPT, bool V4, int Q, bool XY>
@@ -182,7 +182,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, i
         const float ga = er[2];
         if (lane >= n) al = be = 0.f;
         gb += lane < n ? ga : 0.f;
-        const int xsel = XY ? (j == 0 ? a.lay.oX : a.lay.oY) : 0;
+        const int xsel = XY ? (j == 0 ? a.lay.oG1 : a.lay.oG2) : 0;
         const float de = (XY && lane < n && j < 2) ? 1.f : 0.f;
         for (int k0 = 0; k0 < n; k0 += UNR) {
             VT v1[UNR][Q], v2[UNR][Q], v3[XY ? UNR : 1][Q];

@@ -53,9 +53,11 @@ def _assert_params_close(got, want, what):
 
 
 SP_CASES = ["sp_basic", "sp_reg", "sp_sgd_noext"]
+BIL_CASES = ["rescal_basic", "rescal_reg", "hybrid_basic", "hybrid_testpy"]
+ALL_CASES = SP_CASES + BIL_CASES
 
 
-@pytest.mark.parametrize("name", SP_CASES)
+@pytest.mark.parametrize("name", ALL_CASES)
 @pytest.mark.parametrize("graph", [True, False])
 def test_epoch_path_matches_reference_golden(built_lib, cuda_dev, name, graph):
     z, X = _case(name)
@@ -77,7 +79,7 @@ def _assert_labels(lab, z, X):
     assert np.array_equal(lab[clear], z["labels"][:nrow][clear])
 
 
-@pytest.mark.parametrize("name", SP_CASES)
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_func_train_per_call_matches_reference_golden(built_lib, cuda_dev, name):
     """The reference's own call pattern: err += func['train'](b, neg1[:, cols], neg2[:, cols])."""
     z, X = _case(name)
@@ -108,17 +110,25 @@ def _oracle_trajectory(decoder, data, seed, m, r, s, l, epochs, **hp):
     dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10),   # headline K/r/s/l
     dict(N=240, d=500, m=30, r=100, s=10, l=60, ntrue=6),       # config 2 K/r/s
     dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5),          # non-multiple-of-4 (scalar path)
+    dict(N=400, d=300, m=8, r=16, s=4, l=50, ntrue=4, dec="rescal"),
+    dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5, dec="rescal"),
+    dict(N=200, d=2000, m=100, r=200, s=20, l=100, ntrue=10, dec="rescal", epochs=1),  # C5 shape
+    dict(N=400, d=300, m=8, r=16, s=4, l=50, ntrue=4, dec="rescal+sp"),
+    dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5, dec="rescal+sp"),
+    dict(N=200, d=1000, m=30, r=60, s=10, l=100, ntrue=6, dec="rescal+sp"),
 ])
 def test_synthetic_vs_oracle(built_lib, cuda_dev, shape):
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     data, gold = synthetic_dataset(shape["N"], shape["d"], shape["ntrue"], seed=99)
     m, r, s, l = shape["m"], shape["r"], shape["s"], shape["l"]
-    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, l, r, m, s, 0.0, 0.0,
-                             "adagrad", "syn", "sp", False, True, False, 1.0, device=cuda_dev,
+    dec = shape.get("dec", "sp")
+    ep = shape.get("epochs", 2)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), ep, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "syn", dec, False, True, False, 1.0, device=cuda_dev,
                              graph_chunk=2)
     errs = ind.learn(verbose=False)
-    tr, costs = _oracle_trajectory("sp", data, 2, m, r, s, l, 2, lr=0.1, alpha=1.0)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
     got = np.array(ind.epoch_costs)
     np.testing.assert_allclose(got, costs, rtol=COST_RTOL, atol=COST_RTOL)
     _assert_params_close(_params(ind), tr.params, "synthetic")
@@ -167,7 +177,7 @@ def test_label_pass_matches_oracle(built_lib, cuda_dev):
     np.testing.assert_allclose(pr.cpu().numpy(), want_p, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("name", SP_CASES)
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_single_step_each_parameter(built_lib, cuda_dev, name):
     """One func['train'] call: every parameter vs the reference's params after step 1."""
     z, X = _case(name)
