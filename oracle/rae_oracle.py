@@ -285,7 +285,7 @@ def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D):
 
 def train_step_grads(decoder: str, p: dict, X, e1, e2, neg1, neg2, *, alpha: float,
                      lambda1: float = 0.0, lambda2: float = 0.0, adjust: float = 0.0,
-                     ext_reg: bool = True) -> StepResult:
+                     ext_reg: bool = True, denom: float | None = None) -> StepResult:
     """Forward + loss + dense gradients of one ``func['train']`` call.
 
     cost = -mean(all_scores) + lambda1*adjust*L1 + lambda2*adjust*L2
@@ -300,12 +300,14 @@ def train_step_grads(decoder: str, p: dict, X, e1, e2, neg1, neg2, *, alpha: flo
     l = e1.shape[0]
     s = neg1.shape[0]
     D = 4 * l + 2 * l * s
+    if denom is not None:       # data-parallel emulation: a rank's slice of a global batch
+        D = denom
     S, P, logP = encoder_forward(X, p["W"], p["Wb"])
     H = alpha * -(P * logP).sum(axis=1)                     # OieModel.py:81
     pos, negs, dP, g = _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D)
     scores = np.concatenate([pos, H, H, negs])
-    assert scores.shape[0] == D
-    cost = -float(scores.mean())                            # OieModel.py:90
+    assert scores.shape[0] == 4 * l + 2 * l * s
+    cost = -float(scores.sum()) / D                         # OieModel.py:90 (mean)
     # entropy: cost has -(2/D) * sum_b H_b; dH_b/dP_bk = -alpha (logP_bk + 1)
     dP = dP + (2.0 * alpha / D) * (logP + 1.0)
     dS = P * (dP - (P * dP).sum(axis=1, keepdims=True))     # softmax backward

@@ -42,13 +42,25 @@ def init(backend: str | None = None):
 
 
 def make_exchange(world_size: int, rank: int, group=None):
-    """All-gather of the exchange buffer: rank k's slice is rows [k*l, (k+1)*l)."""
+    """All-gather of the exchange buffer: rank k's slice is rows [k*l, (k+1)*l).
+
+    RCCL ("nccl" backend) gathers in place in HBM, stream-ordered, so it can sit inside a
+    captured HIP graph.  The gloo backend (CPU tests; several ranks sharing one GPU) has no
+    device path: the buffer is staged through host memory, which synchronises the stream, so
+    that mode runs eagerly (graph_chunk=1)."""
     if world_size == 1:
         return None
 
     def exchange(buf: torch.Tensor):
         n = buf.numel() // world_size
-        dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n], group=group)
+        if buf.is_cuda and dist.get_backend(group) != "nccl":
+            host = buf.cpu()
+            dist.all_gather_into_tensor(host, host[rank * n:(rank + 1) * n].clone(), group=group)
+            buf.copy_(host)
+        elif not buf.is_cuda:
+            dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n].clone(), group=group)
+        else:
+            dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n], group=group)
 
     return exchange
 
