@@ -30,6 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "relation-autoencoder_amd"))
 
 METRIC = "train examples/sec (fwd+bwd) K=100 d=200 neg=20 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_16x16x4_f32)
 
 # BASELINE.json configs: N triples, feature dim, K, embed, neg, decoder
 CONFIGS = {
@@ -44,17 +45,51 @@ CONFIGS = {
 }
 
 
-def forward_bytes(indptr, ex0, L, m, r, s, rec_floats, dec):
-    """Algorithmic HBM bytes of one forward launch over examples [ex0, ex0+L):
-    per example: CSR indptr+indices 4(f+1), W rows 4*f*m, entity/neg ids + Ab 8(2+2s),
-    A rows 4*r*(1+2s) (SP reads A[e1] and the negatives; RESCAL also A[e2]),
-    exchange record 4*rec; per launch: C1, C2 4*2*r*m, Wb 4m, the row index written
-    (3 int32 per record).  No cross-example reuse credited."""
-    f = np.diff(indptr[ex0:ex0 + L + 1]).astype(np.int64)
-    nrows = (1 + 2 * s) if dec == "sp" else (2 + 2 * s)
-    per_ex = 4 * (f + 1) + 4 * f * m + 8 * (2 + 2 * s) + 4 * r * nrows + 4 * rec_floats
-    per_launch = 4 * 2 * r * m + 4 * m + 12 * (L * (2 + 2 * s) + int(f.sum()))
-    return int(per_ex.sum() + per_launch)
+def step_bytes(host, ex0, L, l, rank, m, r, s, dec):
+    """Algorithmic HBM bytes of one step, split by kernel (SURVEY 8(d) terms; the exchange
+    records and the row index are this design's intermediates and are NOT counted):
+      k_forward (this rank's l examples): per example CSR 4(f+1), W-row gather 4 f m, entity
+        ids 8(1+s), Ab gather 8(1+s), A-row gather 4 r (1+2s) (SP reads A[e1] and the
+        negatives; RESCAL / hybrid also A[e2]); per launch C1, C2 (SP/hybrid) 8 r m, Wb 4 m.
+      k_update (global batch): every distinct referenced row read + written once with its
+        AdaGrad accumulator, 16 B per element: 16 (m U_W + r U_A + U_Ab); dense decoder
+        matrices and Wb 16 (P_dec + m), P_dec = 2rm (SP), r^2 m (RESCAL), r^2 m + 2rm (hybrid).
+    U_W / U_A are counted exactly from the batch's feature ids and entity ids."""
+    indptr = host["indptr"]
+    rows = slice(ex0 + rank * l, ex0 + rank * l + l)
+    f = np.diff(indptr[rows.start:rows.stop + 1]).astype(np.int64)
+    nA = (1 + 2 * s) if dec == "sp" else (2 + 2 * s)
+    fwd = int((4 * (f + 1) + 4 * f * m + 16 * (1 + s) + 4 * r * nA).sum())
+    if dec != "rescal":
+        fwd += 8 * r * m
+    fwd += 4 * m
+    gfe = slice(ex0, ex0 + L)
+    feats = host["indices"][indptr[gfe.start]:indptr[gfe.stop]]
+    ents = np.concatenate([host["args1"][gfe], host["args2"][gfe],
+                           host["neg1"][:, gfe].ravel(), host["neg2"][:, gfe].ravel()])
+    UW, UA = np.unique(feats).size, np.unique(ents).size
+    pdec = {"sp": 2 * r * m, "rescal": r * r * m, "rescal+sp": r * r * m + 2 * r * m}[dec]
+    upd = 16 * (m * UW + r * UA + UA) + 16 * (pdec + m)
+    return fwd, upd
+
+
+def step_flops(L, l, m, r, dec):
+    """MFMA flops of one step for the bilinear decoders: M = P.R (2 l r^2 m), the dP
+    contraction (2 l r^2 m) and the R/C gradient (2 L r^2 m)."""
+    if dec == "sp":
+        return 0
+    return 2 * r * r * m * (2 * l + L)
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/), if any:
+    2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half of a wide
+    coalesced read on gfx950), averaged over the launches of each kernel."""
+    path = os.path.join(ROOT, "profiles", f"r01_{config}_pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh)
 
 
 def cpu_baseline(data, cfg, l, budget_s, seed=2):
@@ -163,25 +198,51 @@ def main():
     n_it = min(args.kernel_iters, nb - b0, eng.index_window)
     lib.rae_build_index(plan, b0, n_it, sp_)
     lib.rae_set_cursor(plan, b0, sp_)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(n_it)]
-    for i, (e0, e1, e2) in enumerate(evs):
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(n_it)]
+    for i, (e0, e1, e2, e3) in enumerate(evs):
         e0.record(st)
         lib.rae_step_forward(plan, i, sp_)
         e1.record(st)
         if exchange is not None:
             exchange(eng.exchange_buf)
-        lib.rae_step_update(plan, i, sp_)
         e2.record(st)
+        lib.rae_step_update(plan, i, sp_)
+        e3.record(st)
     torch.cuda.synchronize()
-    fwd_ms = np.array([a.elapsed_time(b) for a, b, _ in evs])
-    upd_ms = np.array([b.elapsed_time(c) for _, b, c in evs])
+    fwd_ms = np.array([a.elapsed_time(b) for a, b, _, _ in evs])
+    xch_ms = np.array([b.elapsed_time(c) for _, b, c, _ in evs])
+    upd_ms = np.array([c.elapsed_time(d) for _, _, c, d in evs])
     fwd_us = float(np.mean(fwd_ms) * 1e3)
     upd_us = float(np.mean(upd_ms) * 1e3)
-    indptr = eng.split.indptr_np
-    fb = np.mean([forward_bytes(indptr, (b0 + i) * L, L, cfg["m"], cfg["r"], cfg["s"],
-                                eng.rec_floats, cfg["dec"]) for i in range(n_it)])
-    achieved = fb / (fwd_us * 1e-6) / 1e9
+    dec = cfg["dec"]
+    xs = data.split["train"]
+    host = dict(indptr=np.asarray(xs.xFeats.indptr, dtype=np.int64), indices=xs.xFeats.indices,
+                args1=xs.args1, args2=xs.args2, neg1=neg1, neg2=neg2)
+    by = np.array([step_bytes(host, (b0 + i) * L, L, l, rk, cfg["m"], cfg["r"], cfg["s"], dec)
+                   for i in range(n_it)], dtype=np.float64).mean(axis=0)
+    kern = {"k_forward": {"bytes_per_launch": by[0], "avg_launch_us": fwd_us,
+                          "achieved_GBs": by[0] / (fwd_us * 1e-6) / 1e9},
+            "k_update": {"bytes_per_launch": by[1], "avg_launch_us": upd_us,
+                         "achieved_GBs": by[1] / (upd_us * 1e-6) / 1e9}}
+    if dec != "sp":
+        kern["k_forward"]["kernels"] = "k_bil_enc + k_bil_m + k_bil_dec + k_bil_dp + k_bil_fin"
+    traffic = pmc_traffic(args.config)
+    dom = "k_update" if upd_us >= fwd_us else "k_forward"
+    if dec == "sp":
+        ach = kern[dom]["achieved_GBs"]
+        roof = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "traffic": (traffic or {}).get(dom), "bytes_per_launch": kern[dom]["bytes_per_launch"],
+                "avg_launch_us": kern[dom]["avg_launch_us"],
+                "timing": "HIP events around eager launches on the launch stream",
+                "traffic_source": (traffic or {}).get("source")}
+    else:
+        fl = step_flops(L, l, cfg["m"], cfg["r"], dec)
+        ach = fl / ((fwd_us + upd_us) * 1e-6) / 1e12
+        roof = {"kernel": "step (forward phase + k_update)", "bound": "mfma", "achieved": ach,
+                "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / MFMA_F32_PEAK_TFS,
+                "traffic": None, "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
+                "timing": "HIP events around eager launches on the launch stream"}
 
     ms_per_step = 1e3 * elapsed / K
     out = {
@@ -202,12 +263,10 @@ def main():
                    "embed": cfg["r"], "neg_samples": cfg["s"], "decoder": cfg["dec"],
                    "optimizer": "adagrad", "parallelism": f"dp{ws}",
                    "n_entities": data.get_arg_voc_size(), "graph_chunk": args.graph_chunk},
-        "roofline": {"kernel": "k_forward (index WGs + per-example encoder/decoder fwd+bwd)",
-                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "bytes_per_launch": fb, "avg_launch_us": fwd_us,
-                     "timing": "HIP events around eager launches on the launch stream"},
+        "roofline": roof,
+        "kernels": kern,
         "kernel_us": {"forward": fwd_us, "update": upd_us,
+                      "exchange": float(np.mean(xch_ms) * 1e3),
                       "forward_p50": float(np.median(fwd_ms) * 1e3),
                       "update_p50": float(np.median(upd_ms) * 1e3)},
         "negative_sampling_s": t_neg,
