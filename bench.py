@@ -140,6 +140,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
+    ap.add_argument("--no-label-pass", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -244,6 +245,39 @@ def main():
                 "traffic": None, "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
                 "timing": "HIP events around eager launches on the launch stream"}
 
+    # ---- labelling pass over the whole train split (func['label_train'] at full-split scale,
+    # the encoder kernel K1 in inference mode): fixed weights, probs + labels
+    label = None
+    if not args.no_label_pass:
+        split = eng.split
+        Nl = split.N
+        lab = torch.empty(Nl, dtype=torch.int64, device=dev)
+        pr = torch.empty((Nl, cfg["m"]), dtype=torch.float32, device=dev)
+        Wt, Wbt = ind.modelFunc.params[0], ind.modelFunc.params[1]
+
+        def _label():
+            lib.rae_label(C.c_void_p(split.indptr.data_ptr()), C.c_void_p(split.indices.data_ptr()),
+                          None, C.c_void_p(Wt.data_ptr()), C.c_void_p(Wbt.data_ptr()), cfg["m"], 0, Nl,
+                          C.c_void_p(lab.data_ptr()), C.c_void_p(pr.data_ptr()), sp_)
+        _label()
+        torch.cuda.synchronize()
+        le = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(5)]
+        for a_, b_ in le:
+            a_.record(st)
+            _label()
+            b_.record(st)
+        torch.cuda.synchronize()
+        lus = float(np.mean([a_.elapsed_time(b_) for a_, b_ in le]) * 1e3)
+        nnz = int(split.indptr_np[Nl])
+        lbytes = 4 * (Nl + 1) + 4 * nnz + 4 * nnz * cfg["m"] + 4 * Nl * cfg["m"] + 8 * Nl + 4 * cfg["m"]
+        lach = lbytes / (lus * 1e-6) / 1e9
+        label = {"kernel": "k_label (rae_label over the whole train split)", "rows": Nl,
+                 "avg_launch_us": lus, "bytes_per_launch": lbytes, "achieved": lach,
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": lach / HBM_PEAK_GBS,
+                 "rows_per_s": Nl / (lus * 1e-6),
+                 "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label)"}
+        del lab, pr
+
     ms_per_step = 1e3 * elapsed / K
     out = {
         "metric": METRIC,
@@ -269,6 +303,7 @@ def main():
                       "exchange": float(np.mean(xch_ms) * 1e3),
                       "forward_p50": float(np.median(fwd_ms) * 1e3),
                       "update_p50": float(np.median(upd_ms) * 1e3)},
+        "label_pass": label,
         "negative_sampling_s": t_neg,
         "dataset_build_s": t_data,
     }

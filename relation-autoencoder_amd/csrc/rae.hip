@@ -21,6 +21,7 @@
 #include "rae_bilinear.hpp"
 #include "rae_common.hpp"
 #include "rae_index.hpp"
+#include "rae_label.hpp"
 #include "rae_sp.hpp"
 #include "rae_step.hpp"
 #include "rae_update.hpp"
@@ -234,63 +235,6 @@ __global__ void k_set_cursor(int64_t* cursor, int64_t v) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *cursor = v;
 }
 
-// func['label_*']: labels = argmax(S) (first max), probs = softmax(S); one wave per example
-// (RelationClassifier.py:39-48).
-__global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* indptr, const int32_t* indices,
-                                                  const float* values, const float* W,
-                                                  const float* Wb, int m, int64_t row0,
-                                                  int64_t nrows, int64_t* labels, float* probs) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * RAE_NWAVE;
-    for (int64_t e = blockIdx.x * (int64_t)RAE_NWAVE + (threadIdx.x >> 6); e < nrows; e += nw) {
-        const int64_t ex = row0 + e;
-        const int p0 = indptr[ex], p1 = indptr[ex + 1];
-        float S[8];
-#pragma unroll
-        for (int cc = 0; cc < 8; ++cc) S[cc] = 0.f;
-        for (int p = p0; p < p1; ++p) {
-            const int64_t f = indices[p];
-            const float v = values ? values[p] : 1.f;
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) {
-                const int k = lane + 64 * cc;
-                if (k < m) S[cc] += v * W[f * m + k];
-            }
-        }
-        float best = -INFINITY;
-        int bk = 0x7fffffff;
-#pragma unroll
-        for (int cc = 0; cc < 8; ++cc) {
-            const int k = lane + 64 * cc;
-            if (k < m) {
-                S[cc] += Wb[k];
-                if (S[cc] > best) { best = S[cc]; bk = k; }
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ob = __shfl_xor(best, o, 64);
-            const int ok = __shfl_xor(bk, o, 64);
-            if (ob > best || (ob == best && ok < bk)) { best = ob; bk = ok; }
-        }
-        if (lane == 0) labels[e] = bk;
-        if (probs) {
-            float se = 0.f;
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) {
-                const int k = lane + 64 * cc;
-                if (k < m) se += expf(S[cc] - best);
-            }
-            se = wave_sum(se);
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) {
-                const int k = lane + 64 * cc;
-                if (k < m) probs[e * m + k] = expf(S[cc] - best) / se;
-            }
-        }
-    }
-}
-
 // ======================================================================================
 // host side / C ABI
 // ======================================================================================
@@ -366,6 +310,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
          (c.decoder != RAE_DEC_SP && !buf->acc_R3)))
         return fail(RAE_E_INVALID, "AdaGrad accumulators required");
 
+    {
+        const RecLayout lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples);
+        if ((int64_t)lay.rec * c.batch_size * c.world_size >= (1ll << 31))
+            return fail(RAE_E_INVALID, "exchange buffer exceeds 2^31 floats (global batch too large)");
+    }
     rae_plan* p = new rae_plan();
     p->cfg = c;
     p->buf = *buf;
@@ -706,11 +655,18 @@ extern "C" int rae_label(const int32_t* indptr, const int32_t* indices, const fl
                          int64_t* labels, float* probs, rae_stream_t stream) {
     if (!indptr || !indices || !W || !Wb || !labels) return fail(RAE_E_INVALID, "null argument");
     if (m < 1 || m > 512) return fail(RAE_E_INVALID, "relations must be in [1, 512] for labelling");
+    const bool v4 = (m % 4) == 0;
+    if (!v4 && m > 128)
+        return fail(RAE_E_INVALID, "relations must be a multiple of 4 above 128 for labelling");
     if (nrows <= 0) return RAE_OK;
     int64_t blocks = (nrows + RAE_NWAVE - 1) / RAE_NWAVE;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_label, dim3((unsigned)blocks), dim3(RAE_BT), 0, (hipStream_t)stream, indptr,
-                       indices, values, W, Wb, m, row0, nrows, labels, probs);
+    if (v4)
+        hipLaunchKernelGGL(k_label<true>, dim3((unsigned)blocks), dim3(RAE_BT), 0, (hipStream_t)stream,
+                           indptr, indices, values, W, Wb, m, row0, nrows, labels, probs);
+    else
+        hipLaunchKernelGGL(k_label<false>, dim3((unsigned)blocks), dim3(RAE_BT), 0, (hipStream_t)stream,
+                           indptr, indices, values, W, Wb, m, row0, nrows, labels, probs);
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }

@@ -377,7 +377,11 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
             rec[a.lay.odw1 + i] = hybrid ? S.dw1[i] : 0.f;
             rec[a.lay.odw2 + i] = hybrid ? S.dw2[i] : 0.f;
         }
-        for (int j = threadIdx.x; j < 3 * NJ; j += RAE_FBT) rec[a.lay.ocoef + j] = S.coef[j];
+        for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
+            const float* c = S.coef + 3 * j;
+            rec[a.lay.ocoef + 2 * j] = j < 2 ? 1.f : (j < 2 + s ? c[0] : c[1]);
+            rec[a.lay.ocoef + 2 * j + 1] = c[2];
+        }
         if (threadIdx.x == 0) rec[a.lay.oloss] = S.red[32];
     }
 }

@@ -425,13 +425,21 @@ __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, Exa
         rec[a.lay.oP + k] = S.sP[k];
         rec[a.lay.odS + k] = S.sdP[k];
     }
+    const float dl = S.scoef[0], dr = S.scoef[1];
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        rec[a.lay.oV1 + i] = S.swC1[i];
-        rec[a.lay.oV2 + i] = S.swC2[i];
+        const float w1 = S.swC1[i], w2 = S.swC2[i];
+        rec[a.lay.oV1 + i] = w1;
+        rec[a.lay.oV2 + i] = w2;
         rec[a.lay.odw1 + i] = S.sdw1[i];
         rec[a.lay.odw2 + i] = S.sdw2[i];
+        rec[a.lay.oG1 + i] = dl * w1 + dr * w2;        // A[e1]: left and right both read it
     }
-    for (int j = threadIdx.x; j < 3 * NJ; j += RAE_FBT) rec[a.lay.ocoef + j] = S.scoef[j];
+    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
+        const float* c = S.scoef + 3 * j;
+        const float cj = j == 0 ? 1.f : (j == 1 ? 0.f : (j < 2 + Dm.s ? c[0] : c[1]));
+        rec[a.lay.ocoef + 2 * j] = cj;
+        rec[a.lay.ocoef + 2 * j + 1] = c[2];
+    }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
 }
 

@@ -5,20 +5,22 @@
 namespace rae {
 
 // Per-example record in the exchange buffer (floats).
-//   P (m) | dS (m) | V1 (r) | V2 (r) | dw1 (r) | dw2 (r) |
-//   [bilinear: G1 (r) | G2 (r) | X (r) | Y (r) | A1 (r) | A2 (r) | z = S - max S (m)] |
-//   coef (3*NJ) | loss (1) | pad
-// coef[j] = (alpha_j, beta_j, gamma_j) for record j (0: e1, 1: e2, 2..: neg1[t], neg2[t]):
-// record j's A-row gradient is alpha_j*V1 + beta_j*V2 (+ G1 for j = 0, G2 for j = 1 on the
-// bilinear decoders) and its Ab gradient gamma_j.
-// SP       : V1 = wC1 = C1.P, V2 = wC2, dw1/dw2 = dCost/dwC1, dCost/dwC2.
+//   P (m) | dS (m) | V1 (r) | V2 (r) | dw1 (r) | dw2 (r) | G1 (r) |
+//   [bilinear: G2 (r) | X (r) | Y (r) | A1 (r) | A2 (r) | z = S - max S (m)] |
+//   coef (2*NJ) | loss (1) | pad
+// coef[j] = (c_j, gamma_j) for record j (0: e1, 1: e2, 2+t: neg1[t], 2+s+t: neg2[t]):
+// record j's A-row gradient is c_j * vec_j and its Ab gradient gamma_j, with
+// vec_0 = G1, vec_1 = G2 (bilinear; SP: c_1 = 0), vec_{neg1} = V1, vec_{neg2} = V2 -- one
+// vector per record, so the update reads exactly one r-vector per referencing record.
+// SP       : V1 = wC1 = C1.P, V2 = wC2, G1 = dl*wC1 + dr*wC2 (e1's whole A gradient),
+//            dw1/dw2 = dCost/dwC1, dCost/dwC2.
 // bilinear : V1 = M a2 (+ wC1), V2 = M^T a1 (+ wC2) with M = sum_k P_k R[:,:,k];
 //            G1/G2 = the full A-row gradients of e1/e2; X, Y, A1, A2 the rank-2 factors of
 //            dCost/dM = X A2^T + A1 Y^T (A1/A2 = copies of A[e1], A[e2] taken before the
 //            update kernel changes A); dw1/dw2 as SP for the hybrid.
 struct RecLayout {
-    int oP, odS, oV1, oV2, odw1, odw2, ocoef, oloss, rec;
-    int oG1, oG2, oX, oY, oA1, oA2, oZ;   // bilinear decoders only (0 for SP)
+    int oP, odS, oV1, oV2, odw1, odw2, oG1, ocoef, oloss, rec;
+    int oG2, oX, oY, oA1, oA2, oZ;   // bilinear decoders only (0 for SP)
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
@@ -33,9 +35,9 @@ __host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s) {
     L.oV2 = L.oV1 + r4;
     L.odw1 = L.oV2 + r4;
     L.odw2 = L.odw1 + r4;
-    int o = L.odw2 + r4;
+    L.oG1 = L.odw2 + r4;
+    int o = L.oG1 + r4;
     if (dec != 0) {
-        L.oG1 = o; o += r4;
         L.oG2 = o; o += r4;
         L.oX = o; o += r4;
         L.oY = o; o += r4;
@@ -44,7 +46,7 @@ __host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s) {
         L.oZ = o; o += m4;
     }
     L.ocoef = o;
-    o += align4(3 * NJ);
+    o += align4(2 * NJ);
     L.oloss = o;
     L.rec = align4(o + 1);
     return L;

@@ -149,16 +149,17 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 }
 
 // ---- A / Ab rows -------------------------------------------------------------------------
-// g(A[e]) = sum over the row's records (in sorted order) of
-//   alpha_j * V1_b + beta_j * V2_b (+ G1_b for j = 0 / G2_b for j = 1 when XY: bilinear)
-// g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per record),
-// the record vectors RAE_UNR at a time with every load issued before the first FMA.
+// g(A[e]) = sum over the row's records (in sorted order) of c_j * vec_j (rae_step.hpp: one
+// r-vector per record: G1 for e1, G2 for e2 on the bilinear decoders, V1 for neg1, V2 for
+// neg2), g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per
+// record) and broadcast with v_readlane (wave-uniform -> scalar addressing); the record
+// vectors are loaded UNR at a time with every load issued before the first FMA.
 template <int OPT, bool V4, int Q, bool XY>
 __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, int C, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? 8 : 4;
     typedef typename VecT<V4>::T VT;
-    const int r = a.r, nv = r / VW, NJ = 2 + 2 * a.s;
+    const int r = a.r, nv = r / VW, s = a.s, NJ = 2 + 2 * s;
     const int64_t base = slot * a.RA;
     const int2 seg = reinterpret_cast<const int2*>(a.urowA + 2 * base)[u];
     const int nxt = a.urowA[2 * base + 2 * (u + 1 < U ? u + 1 : u) + 1];
@@ -173,56 +174,38 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, i
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
     g.zero();
     float gb = 0.f;
+    const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;   // SP: e2 has no A gradient (c = 0)
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
         const int rec = a.srecA[base + c0 + (lane < n ? lane : 0)];
         const int b = rec / NJ, j = rec - b * NJ;
-        const float* er = a.ex + (int64_t)b * a.lay.rec + a.lay.ocoef + 3 * j;
-        float al = er[0], be = er[1];
-        const float ga = er[2];
-        if (lane >= n) al = be = 0.f;
+        const int rb = b * a.lay.rec;
+        const float* er = a.ex + rb + a.lay.ocoef + 2 * j;
+        float cj = er[0];
+        const float ga = er[1];
+        if (lane >= n) cj = 0.f;
         gb += lane < n ? ga : 0.f;
-        const int xsel = XY ? (j == 0 ? a.lay.oG1 : a.lay.oG2) : 0;
-        const float de = (XY && lane < n && j < 2) ? 1.f : 0.f;
+        const int vo = rb + (j == 0 ? a.lay.oG1 : (j == 1 ? vo1 : (j < 2 + s ? a.lay.oV1 : a.lay.oV2)));
         for (int k0 = 0; k0 < n; k0 += UNR) {
-            VT v1[UNR][Q], v2[UNR][Q], v3[XY ? UNR : 1][Q];
-            float cal[UNR], cbe[UNR], cde[UNR];
+            VT v[UNR][Q];
+            float ck[UNR];
 #pragma unroll
             for (int k = 0; k < UNR; ++k) {
                 const int src = min(k0 + k, RAE_WAVE - 1);
-                const int bk = __shfl(b, src, 64);
-                cal[k] = (k0 + k < n) ? __shfl(al, src, 64) : 0.f;
-                cbe[k] = (k0 + k < n) ? __shfl(be, src, 64) : 0.f;
-                const float* rk = a.ex + (int64_t)bk * a.lay.rec;
-                const VT* V1 = reinterpret_cast<const VT*>(rk + a.lay.oV1);
-                const VT* V2 = reinterpret_cast<const VT*>(rk + a.lay.oV2);
+                const int ok = __builtin_amdgcn_readlane(vo, src);
+                ck[k] = (k0 + k < n) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj), src))
+                                     : 0.f;
+                const VT* V = reinterpret_cast<const VT*>(a.ex + ok);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;
-                    const int cs = c < nv ? c : 0;
-                    v1[k][q] = V1[cs];
-                    v2[k][q] = V2[cs];
-                }
-                if (XY) {
-                    cde[k] = (k0 + k < n) ? __shfl(de, src, 64) : 0.f;
-                    const int xk = __shfl(xsel, src, 64);
-                    const VT* V3 = reinterpret_cast<const VT*>(rk + xk);
-#pragma unroll
-                    for (int q = 0; q < Q; ++q) {
-                        const int c = lane + RAE_WAVE * q;
-                        v3[XY ? k : 0][q] = V3[c < nv ? c : 0];
-                    }
+                    v[k][q] = V[c < nv ? c : 0];
                 }
             }
 #pragma unroll
-            for (int k = 0; k < UNR; ++k) {
+            for (int k = 0; k < UNR; ++k)
 #pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    vfma(g.v[q], cal[k], v1[k][q]);
-                    vfma(g.v[q], cbe[k], v2[k][q]);
-                    if (XY) vfma(g.v[q], cde[k], v3[XY ? k : 0][q]);
-                }
-            }
+                for (int q = 0; q < Q; ++q) vfma(g.v[q], ck[k], v[k][q]);
         }
     }
     gb = wave_sum(gb);
@@ -269,9 +252,10 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
 #pragma unroll
             for (int k = 0; k < UNR; ++k) {
                 const int src = min(k0 + k, RAE_WAVE - 1);
-                const int bk = __shfl(b, src, 64);
-                cv[k] = (k0 + k < n) ? __shfl(val, src, 64) : 0.f;
-                const VT* dS = reinterpret_cast<const VT*>(a.ex + (int64_t)bk * a.lay.rec + a.lay.odS);
+                const int bk = __builtin_amdgcn_readlane(b, src);
+                cv[k] = (k0 + k < n) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val), src))
+                                     : 0.f;
+                const VT* dS = reinterpret_cast<const VT*>(a.ex + bk * a.lay.rec + a.lay.odS);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;

@@ -92,6 +92,44 @@ class DatasetManager:
 
 
 # ---------------------------------------------------------------------------------------
+# on-disk format (numpy .npz, no pickles): the arrays of every split + entity frequencies
+# ---------------------------------------------------------------------------------------
+def save_npz(path, data: DatasetManager, gold_standard=None):
+    """Write a DatasetManager (+ gold standard {split: {index: [label, ...]}}) as .npz."""
+    out = {"n_features": np.int64(data.n_features), "entity_freqs": data.entity_freqs,
+           "power": np.float64(data.negSamplingDistrPower)}
+    for name, sp_ in data.split.items():
+        x = sp_.xFeats
+        out[f"{name}/indptr"] = np.asarray(x.indptr, dtype=np.int64)
+        out[f"{name}/indices"] = np.asarray(x.indices, dtype=np.int32)
+        out[f"{name}/data"] = np.asarray(x.data, dtype=np.float32)
+        out[f"{name}/args1"] = sp_.args1
+        out[f"{name}/args2"] = sp_.args2
+        g = (gold_standard or {}).get(name) or {}
+        idx = np.array(sorted(g), dtype=np.int64)
+        out[f"{name}/gold_index"] = idx
+        out[f"{name}/gold_label"] = np.array([str(g[int(i)][0]) for i in idx], dtype=np.str_)
+    np.savez(path, **out)
+
+
+def load_npz(path):
+    """Inverse of save_npz -> (DatasetManager, gold standard).  allow_pickle stays False."""
+    z = np.load(path, allow_pickle=False)
+    d = int(z["n_features"])
+    splits, gold = {}, {}
+    for name in SPLIT_LABELS:
+        if f"{name}/indptr" not in z:
+            continue
+        indptr = z[f"{name}/indptr"]
+        X = sp.csr_matrix((z[f"{name}/data"], z[f"{name}/indices"], indptr),
+                          shape=(len(indptr) - 1, d))
+        splits[name] = DatasetSplit(z[f"{name}/args1"], z[f"{name}/args2"], X)
+        gold[name] = {int(i): [str(lbl)] for i, lbl in zip(z[f"{name}/gold_index"],
+                                                              z[f"{name}/gold_label"])}
+    return DatasetManager(splits, z["entity_freqs"], d, float(z["power"])), gold
+
+
+# ---------------------------------------------------------------------------------------
 # synthetic (e1, e2, feature-bag) triples, SURVEY.md 8d
 # ---------------------------------------------------------------------------------------
 def _zipf_sampler(rng, n, a, size):

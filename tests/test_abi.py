@@ -28,9 +28,14 @@ def test_struct_layout_matches_header(built_lib):
     cfg = _lib.RaeConfig()
     cfg.decoder, cfg.relations, cfg.embed, cfg.neg_samples = 0, 100, 200, 20
     cfg.batch_size, cfg.world_size = 100, 1
-    # record layout: P, dS (m) + V1, V2, dw1, dw2 (r) + coef 3*(2+2s) + loss, 16-B aligned
+    # record layout (rae_step.hpp): P, dS (m) + V1, V2, dw1, dw2, G1 (r) + coef 2*(2+2s) + loss,
+    # 16-B aligned
     rec = built_lib.rae_exchange_record_floats(C.byref(cfg))
-    assert rec == ((2 * 100 + 4 * 200 + ((3 * 42 + 3) & ~3) + 1 + 3) & ~3)
+    assert rec == ((2 * 100 + 5 * 200 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
+    cfg.decoder = 1     # bilinear: + G2, X, Y, A1, A2 (r) + z (m)
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == \
+        ((3 * 100 + 10 * 200 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
+    cfg.decoder = 0
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 100
     cfg.world_size = 8
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 800

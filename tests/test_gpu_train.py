@@ -196,3 +196,21 @@ def test_single_step_each_parameter(built_lib, cuda_dev, name):
             bad.append(f"{k}: max err {err.max():.3e} at {idx} got {got[k][idx]:.6g} "
                        f"want {z['step1_' + k][idx]:.6g} init {z['init_' + k][idx]:.6g}")
     assert not bad, "; ".join(bad)
+
+
+@pytest.mark.parametrize("decoder", ["sp", "rescal+sp"])
+def test_cli_end_to_end(built_lib, cuda_dev, decoder):
+    """python -m rae (the OieInduction.py command line) trains on the GPU end to end."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    env = dict(os.environ)
+    env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, "-m", "rae", "synthetic:1000:2000:5", "--model-name", "t",
+                        "--decoder", decoder, "--epochs", "2", "--batch-size", "100",
+                        "--relations", "10", "--embed-size", "16", "--neg-samples", "4"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    errs = [float(line.split(":")[1]) for line in p.stdout.splitlines()
+            if line.startswith("Training error")]
+    assert len(errs) == 2 and all(np.isfinite(errs))

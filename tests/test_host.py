@@ -1,0 +1,72 @@
+"""Host-side pieces that need no GPU: the command line (learning/OieInduction.py:461-500 and
+the README aliases), the .npz dataset format, batch sizing, and the product path's refusal to
+run without the HIP library."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from rae import cli
+from rae.data import batch_nnz_stats, load_npz, save_npz, synthetic_dataset
+
+
+def test_cli_flags_and_defaults_match_reference():
+    a = cli.get_command_args(["data.npz", "--model-name", "m", "--decoder", "sp"])
+    # learning/OieInduction.py:464-480 defaults
+    assert (a.epochs, a.learning_rate, a.batch_size, a.embed_size, a.relations, a.neg_samples,
+            a.l1, a.l2, a.optimizer, a.alpha, a.seed) == (100, 0.1, 50, 30, 3, 5, 0.0, 0.0,
+                                                           "adagrad", 1.0, 2)
+    assert a.ext_reg is True and a.ext_emb is False and a.freq_eval is False
+
+
+def test_cli_readme_aliases():
+    # README.md:44 / BASELINE.json config 1
+    a = cli.get_command_args(["--pickled_dataset", "x.npz", "--model_name", "discrete-autoencoder",
+                              "--decoder", "sp", "--optimization", "1", "--epochs", "10",
+                              "--batch_size", "100", "--relations_number", "10",
+                              "--negative_samples_number", "5", "--l2_regularization", "0.1",
+                              "--alpha", "0.1", "--seed", "2", "--embed_size", "10",
+                              "--learning_rate", "0.1"])
+    assert (a.dataset, a.model_name, a.optimizer, a.epochs, a.batch_size, a.relations,
+            a.neg_samples, a.l2, a.alpha, a.embed_size) == ("x.npz", "discrete-autoencoder",
+                                                            "adagrad", 10, 100, 10, 5, 0.1, 0.1, 10)
+
+
+def test_cli_requires_model_name_and_decoder():
+    with pytest.raises(SystemExit):
+        cli.get_command_args(["d.npz", "--decoder", "sp"])
+    with pytest.raises(SystemExit):
+        cli.get_command_args(["d.npz", "--model-name", "x"])
+    with pytest.raises(SystemExit):
+        cli.get_command_args(["d.npz", "--model-name", "x", "--decoder", "bogus"])
+
+
+def test_npz_round_trip(tmp_path):
+    data, gold = synthetic_dataset(500, 700, 4, seed=3)
+    p = tmp_path / "ds.npz"
+    save_npz(p, data, gold)
+    d2, g2 = load_npz(p)
+    x1, x2 = data.split["train"].xFeats, d2.split["train"].xFeats
+    assert (x1 != x2).nnz == 0
+    assert np.array_equal(data.split["train"].args1, d2.split["train"].args1)
+    assert np.array_equal(data.negSamplingCum, d2.negSamplingCum)
+    assert g2 == gold
+
+
+def test_batch_nnz_stats():
+    indptr = np.array([0, 3, 4, 9, 10, 12])
+    assert batch_nnz_stats(indptr, 2) == (6, 5)     # batches [0,2) -> 4, [2,4) -> 6; max row 5
+
+
+def test_product_path_fails_loudly_without_library(tmp_path):
+    code = ("import os, sys; os.environ['RAE_LIB'] = os.path.join(sys.argv[1], 'missing.so');"
+            "sys.path.insert(0, sys.argv[2]);"
+            "from rae import _lib\n"
+            "try:\n    _lib.load()\nexcept _lib.RaeError as e:\n    print('refused', e)\n")
+    out = subprocess.run([sys.executable, "-c", code, str(tmp_path),
+                          os.path.join(os.path.dirname(os.path.dirname(__file__)),
+                                       "relation-autoencoder_amd")],
+                         capture_output=True, text=True, timeout=120)
+    assert "refused" in out.stdout, out.stdout + out.stderr
