@@ -122,7 +122,8 @@ class ReconstructInducer:
     def compile_function(self):
         """OieInduction.py:118-155: build the train function and one labelling function
         per split."""
-        self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)   # :137
+        if self.optimizer is None:          # (kept when a checkpoint was loaded first)
+            self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)   # :137
         self.engine = TrainEngine(self.modelFunc, self.optimizer, self.data.split["train"],
                                   learning_rate=self.learningRate, lambda1=self.lambdaL1,
                                   lambda2=self.lambdaL2, world_size=self.world_size,
@@ -166,7 +167,7 @@ class ReconstructInducer:
         if not self._check_for_compiled_functions():
             self.compile_function()
         nb = self.batch_reps["train"]
-        epoch = 0
+        epoch = self.cur_epoch                  # 0, or the epoch a checkpoint was taken at
         while epoch < self.nb_epochs:
             t0 = time.perf_counter()
             epoch += 1
@@ -237,11 +238,46 @@ class ReconstructInducer:
         raise Exception("Either 'train' split or 'train', 'valid' and 'test' splits should be defined")
 
     def state_dict(self):
-        """Parameters + AdaGrad accumulators + RNG state (the reference's save() drops the
-        accumulators, OieInduction.py:110-116)."""
+        """Parameters + AdaGrad accumulators + RNG state + epoch cursor (the reference's
+        save() keeps only the parameters and loses the accumulators and the RNG position,
+        OieInduction.py:110-116, so a reloaded model cannot continue the same run)."""
         sd = {"params": {k: v.detach().cpu() for k, v in self.modelFunc.named_params().items()},
-              "rng": self.rng.get_state(), "epoch": self.cur_epoch}
+              "rng": self.rng.get_state(), "epoch": self.cur_epoch,
+              "train_errors": list(self.train_errors)}
         if self.optimizer is not None and self.optimizer.accumulator is not None:
             sd["acc"] = {k: v.detach().cpu() for k, v in
                          zip(self.modelFunc.param_names, self.optimizer.accumulator)}
         return sd
+
+    def save_checkpoint(self, path):
+        """state_dict() as a flat .npz (no pickles)."""
+        sd = self.state_dict()
+        name, key, pos, has_gauss, gauss = sd["rng"]
+        out = {"epoch": np.int64(sd["epoch"]), "train_errors": np.array(sd["train_errors"]),
+               "rng_key": key, "rng_pos": np.int64(pos), "rng_has_gauss": np.int64(has_gauss),
+               "rng_gauss": np.float64(gauss), "decoder": np.str_(self.decoder_type)}
+        for k, v in sd["params"].items():
+            out["param/" + k] = v.numpy()
+        for k, v in sd.get("acc", {}).items():
+            out["acc/" + k] = v.numpy()
+        np.savez(path, **out)
+
+    def load_checkpoint(self, path):
+        """Restore a save_checkpoint() file into this inducer (same shapes/decoder): the
+        parameters and accumulators are copied into the existing device tensors (a built
+        engine keeps its pointers), the shared RNG resumes its stream and learn() continues
+        at the next epoch."""
+        z = np.load(path, allow_pickle=False)
+        if str(z["decoder"]) != self.decoder_type:
+            raise ValueError(f"checkpoint decoder {z['decoder']} != {self.decoder_type}")
+        for k, v in self.modelFunc.named_params().items():
+            v.copy_(torch.as_tensor(z["param/" + k]))
+        if self.optimizer is None and self.optimization is not None:
+            self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)
+        if self.optimizer is not None and self.optimizer.accumulator is not None:
+            for k, v in zip(self.modelFunc.param_names, self.optimizer.accumulator):
+                v.copy_(torch.as_tensor(z["acc/" + k]))
+        self.rng.set_state(("MT19937", z["rng_key"], int(z["rng_pos"]), int(z["rng_has_gauss"]),
+                            float(z["rng_gauss"])))
+        self.cur_epoch = int(z["epoch"])
+        self.train_errors = [float(x) for x in z["train_errors"]]

@@ -214,3 +214,27 @@ def test_cli_end_to_end(built_lib, cuda_dev, decoder):
     errs = [float(line.split(":")[1]) for line in p.stdout.splitlines()
             if line.startswith("Training error")]
     assert len(errs) == 2 and all(np.isfinite(errs))
+
+
+def test_checkpoint_resume_is_bit_identical(built_lib, cuda_dev, tmp_path):
+    """2 epochs straight == 1 epoch, checkpoint, a fresh inducer loads it, 1 more epoch."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    data, gold = synthetic_dataset(600, 900, 5, seed=8)
+
+    def make(epochs):
+        return ReconstructInducer(data, gold, np.random.RandomState(2), epochs, 0.1, 50, 16, 8, 4,
+                                  0.0, 0.0, "adagrad", "ck", "sp", False, True, False, 1.0,
+                                  device=cuda_dev, graph_chunk=4)
+    a = make(2)
+    a.learn(verbose=False)
+    b = make(1)
+    b.learn(verbose=False)
+    b.save_checkpoint(tmp_path / "ck.npz")
+    c = make(2)
+    c.load_checkpoint(tmp_path / "ck.npz")
+    c.learn(verbose=False)
+    pa, pc = _params(a), _params(c)
+    for k in pa:
+        assert np.array_equal(pa[k], pc[k]), k
+    assert a.train_errors == c.train_errors

@@ -70,3 +70,33 @@ def test_product_path_fails_loudly_without_library(tmp_path):
                                        "relation-autoencoder_amd")],
                          capture_output=True, text=True, timeout=120)
     assert "refused" in out.stdout, out.stdout + out.stderr
+
+
+def test_checkpoint_round_trip_cpu(tmp_path):
+    """Params, AdaGrad accumulators, the shared RNG position and the epoch cursor survive a
+    save/load (the reference's save() keeps only the parameters, OieInduction.py:110-116)."""
+    import torch
+    from rae.inducer import ReconstructInducer
+    data, gold = synthetic_dataset(300, 400, 3, seed=5)
+
+    def make():
+        return ReconstructInducer(data, gold, np.random.RandomState(2), 3, 0.1, 50, 8, 5, 3, 0.0,
+                                  0.0, "adagrad", "ck", "rescal+sp", False, True, False, 1.0,
+                                  device=torch.device("cpu"))
+    a = make()
+    from rae.model import make_optimizer
+    a.optimizer = make_optimizer("adagrad", a.modelFunc.params)
+    g = torch.Generator().manual_seed(0)
+    for t in a.modelFunc.params + a.optimizer.accumulator:
+        t.add_(torch.rand(t.shape, generator=g))
+    a.rng.uniform(size=17)
+    a.cur_epoch, a.train_errors = 1, [3.5]
+    a.save_checkpoint(tmp_path / "ck.npz")
+    b = make()
+    b.load_checkpoint(tmp_path / "ck.npz")
+    for (k, x), y in zip(a.modelFunc.named_params().items(), b.modelFunc.params):
+        assert torch.equal(x, y), k
+    for x, y in zip(a.optimizer.accumulator, b.optimizer.accumulator):
+        assert torch.equal(x, y)
+    assert b.cur_epoch == 1 and b.train_errors == [3.5]
+    assert np.array_equal(a.rng.uniform(size=5), b.rng.uniform(size=5))
