@@ -166,10 +166,14 @@ def main():
                              graph_chunk=args.graph_chunk)
     ind.compile_function()
     eng = ind.engine
+    # per-epoch negatives: the reference's RandomState stream, CDF search on the device
+    # (parity mode, rae_neg_sample) -- timed separately, outside the metric
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    neg1, neg2 = ind.draw_epoch_negatives()
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    torch.cuda.synchronize()
     t_neg = time.perf_counter() - t0
-    eng.set_epoch_negatives(neg1, neg2)
+    neg1, neg2 = eng.neg1.cpu().numpy(), eng.neg2.cpu().numpy()
     rdist.warm_up(exchange, eng.exchange_buf)
     nb = eng.nb
     K, W = args.steps, args.warmup
@@ -305,6 +309,7 @@ def main():
                       "update_p50": float(np.median(upd_ms) * 1e3)},
         "label_pass": label,
         "negative_sampling_s": t_neg,
+        "negative_sampling": "host RandomState uniforms (reference stream) + device CDF search",
         "dataset_build_s": t_data,
     }
     if rk == 0 and ws == 1 and not args.no_cpu_baseline:

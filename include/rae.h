@@ -151,6 +151,18 @@ int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,
 /* Device error word (overflow flags); host reads it with rae_check(). */
 int rae_check(rae_plan* plan);
 
+/* --- negative sampling (learning/NegativeExampleGenerator.py:14-32) ----------------- */
+/* out[i] = first j with cum[j] >= x_i  (numpy searchsorted side='left' over the float64 CDF
+ * negSamplingCum, learning/OieData.py:57-59), i < count, int32.
+ * rae_neg_sample:        x_i = uniforms[i], the caller's draws of U(0, cum[n-1]) -- with the
+ *                        model's RandomState stream this is the reference sampler bit for bit.
+ * rae_neg_sample_philox: x_i = cum[n-1] * U_i, U_i from Philox4x32-10 at counter offset + i
+ *                        under key seed (device-only perf mode, not the reference's stream). */
+int rae_neg_sample(const double* cum_dev, int64_t n, const double* uniforms_dev, int64_t count,
+                   int32_t* out_dev, rae_stream_t stream);
+int rae_neg_sample_philox(const double* cum_dev, int64_t n, uint64_t seed, uint64_t offset,
+                          int64_t count, int32_t* out_dev, rae_stream_t stream);
+
 /* --- labelling (func['label_<split>'], RelationClassifier.py:39-48) ----------------- */
 /* rows [row0, row0+nrows) of any CSR split with the current W/Wb: labels = argmax(S)
  * (int64, first max) and probs = softmax(S) (fp32, may be NULL).                        */

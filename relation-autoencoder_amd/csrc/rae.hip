@@ -22,6 +22,7 @@
 #include "rae_common.hpp"
 #include "rae_index.hpp"
 #include "rae_label.hpp"
+#include "rae_sampler.hpp"
 #include "rae_sp.hpp"
 #include "rae_step.hpp"
 #include "rae_update.hpp"
@@ -648,6 +649,32 @@ extern "C" int rae_check(rae_plan* p) {
     if (e) return fail(RAE_E_OVERFLOW, "row-index partition overflowed its LDS capacity (flags=" +
                                            std::to_string(e) + ")");
     return RAE_OK;
+}
+
+static int launch_neg(const double* cum, int64_t n, const double* u, uint64_t seed,
+                      uint64_t offset, int64_t count, int32_t* out, hipStream_t st, bool philox) {
+    if (!cum || !out || (!philox && !u)) return fail(RAE_E_INVALID, "null argument");
+    if (n < 1 || n >= (1ll << 31)) return fail(RAE_E_INVALID, "CDF size must be in [1, 2^31)");
+    if (count <= 0) return RAE_OK;
+    int64_t blocks = (count + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (philox)
+        hipLaunchKernelGGL(k_neg_sample<true>, dim3((unsigned)blocks), dim3(256), 0, st, cum, n, u,
+                           seed, offset, count, out);
+    else
+        hipLaunchKernelGGL(k_neg_sample<false>, dim3((unsigned)blocks), dim3(256), 0, st, cum, n, u,
+                           seed, offset, count, out);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+
+extern "C" int rae_neg_sample(const double* cum, int64_t n, const double* u, int64_t count,
+                              int32_t* out, rae_stream_t stream) {
+    return launch_neg(cum, n, u, 0, 0, count, out, (hipStream_t)stream, false);
+}
+extern "C" int rae_neg_sample_philox(const double* cum, int64_t n, uint64_t seed, uint64_t offset,
+                                     int64_t count, int32_t* out, rae_stream_t stream) {
+    return launch_neg(cum, n, nullptr, seed, offset, count, out, (hipStream_t)stream, true);
 }
 
 extern "C" int rae_label(const int32_t* indptr, const int32_t* indices, const float* values,

@@ -24,6 +24,7 @@ EXPORTS = (
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
     "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
+    "rae_neg_sample", "rae_neg_sample_philox",
 )
 
 
@@ -89,7 +90,9 @@ def load(path: str | None = None):
     lib.rae_index_window.argtypes = [_P]
     lib.rae_index_window.restype = C.c_int64
     lib.rae_label.argtypes = [_P, _P, _P, _P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, _P]
-    for fn in ("rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
+    lib.rae_neg_sample.argtypes = [_P, C.c_int64, _P, C.c_int64, _P, _P]
+    lib.rae_neg_sample_philox.argtypes = [_P, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, _P, _P]
+    for fn in ("rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
                "rae_check", "rae_label", "rae_build_index"):
         getattr(lib, fn).restype = C.c_int

@@ -53,7 +53,7 @@ class ReconstructInducer:
                  embed_size, nb_relations, nb_neg_samples, lambda1, lambda2, optimization,
                  model_name, decoder_model, external_embeddings, extended_regularizer,
                  frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
-                 graph_chunk=64):
+                 graph_chunk=64, neg_sampler="device", neg_seed=0):
         self.data = data
         self.goldStandard = gold_standard
         self.rng = rng
@@ -77,6 +77,10 @@ class ReconstructInducer:
         self.rank = int(rank)
         self.exchange = exchange
         self.graph_chunk = graph_chunk
+        if neg_sampler not in ("host", "device", "philox"):
+            raise ValueError("neg_sampler must be 'host', 'device' or 'philox'")
+        self.neg_sampler = neg_sampler     # host / device: the reference's RNG stream
+        self.neg_seed = int(neg_seed)
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
                         f"_embedsize{embed_size}_l1{lambda1}_l2{lambda2}_opt{optimization}"
@@ -172,8 +176,12 @@ class ReconstructInducer:
             t0 = time.perf_counter()
             epoch += 1
             self.cur_epoch = epoch
-            neg1, neg2 = self.draw_epoch_negatives()
-            self.engine.set_epoch_negatives(neg1, neg2)
+            if self.neg_sampler == "host":
+                neg1, neg2 = self.draw_epoch_negatives()
+                self.engine.set_epoch_negatives(neg1, neg2)
+            else:
+                self.engine.sample_epoch_negatives(self.negativeSampler, self.neg_sampler,
+                                                   self.neg_seed, epoch - 1)
             if self.frequentEval:
                 # per-batch evaluation needs the host between batches (:190-198)
                 for b in range(nb):

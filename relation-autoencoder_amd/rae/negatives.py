@@ -25,5 +25,14 @@ class NegativeExampleGenerator:
             (num_negative_samples, num_positive_entities))
 
     def _get_sample(self, num_samples: int):
-        u = self._rand.uniform(0, self._negSamplingCum[-1], num_samples)
+        u = self.draw_uniforms(num_samples)
         return np.asarray(self._negSamplingCum.searchsorted(u), dtype=np.int32)
+
+    def draw_uniforms(self, num_samples: int) -> np.ndarray:
+        """The float64 draws of one get_negative_samples call (NegativeExampleGenerator.py:
+        32): U(0, cum[-1]) from the shared RandomState -- the device sampler searches them."""
+        return self._rand.uniform(0, self._negSamplingCum[-1], num_samples)
+
+    @property
+    def cum(self) -> np.ndarray:
+        return self._negSamplingCum
