@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "relation-autoencoder_amd"))
 METRIC = "train examples/sec (fwd+bwd) K=100 d=200 neg=20 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_16x16x4_f32)
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 # BASELINE.json configs: N triples, feature dim, K, embed, neg, decoder
 CONFIGS = {
@@ -40,8 +41,8 @@ CONFIGS = {
                name="C3 synthetic 1M triples K=100 embed=200 neg=20 sp (headline)"),
     "c4": dict(N=10_000_000, d=2 ** 20, m=300, r=300, s=50, dec="sp", ntrue=300,
                name="C4 synthetic 10M triples K=300 embed=300 neg=50 sp"),
-    "c5": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="rescal", ntrue=100,
-               name="C5 synthetic 1M triples K=100 embed=200 neg=20 rescal"),
+    "c5": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="rescal", ntrue=100, bf16=True,
+               name="C5 synthetic 1M triples K=100 embed=200 neg=20 rescal, bf16 MFMA"),
 }
 
 
@@ -163,7 +164,7 @@ def main():
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, cfg["r"], cfg["m"],
                              cfg["s"], 0.0, 0.0, "adagrad", "bench", cfg["dec"], False, True, False,
                              1.0, device=dev, world_size=ws, rank=rk, exchange=exchange,
-                             graph_chunk=args.graph_chunk)
+                             graph_chunk=args.graph_chunk, mfma_bf16=cfg.get("bf16", False))
     ind.compile_function()
     eng = ind.engine
     # per-epoch negatives: the reference's RandomState stream, CDF search on the device
@@ -243,9 +244,10 @@ def main():
                 "traffic_source": (traffic or {}).get("source")}
     else:
         fl = step_flops(L, l, cfg["m"], cfg["r"], dec)
+        pk = MFMA_BF16_PEAK_TFS if cfg.get("bf16") else MFMA_F32_PEAK_TFS
         ach = fl / ((fwd_us + upd_us) * 1e-6) / 1e12
         roof = {"kernel": "step (forward phase + k_update)", "bound": "mfma", "achieved": ach,
-                "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / MFMA_F32_PEAK_TFS,
+                "peak": pk, "unit": "TFLOP/s", "frac": ach / pk,
                 "traffic": None, "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
                 "timing": "HIP events around eager launches on the launch stream"}
 
@@ -294,7 +296,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16 MFMA operands, fp32 accumulate" if cfg.get("bf16") else "fp32",
         "data": "synthetic (SURVEY 8d generator, seed 1234; random-init params, seed 2)",
         "config": {"workload": cfg["name"], "global_batch": L, "batch_per_gpu": l,
                    "n_examples": cfg["N"], "n_features": cfg["d"], "relations": cfg["m"],

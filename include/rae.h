@@ -79,6 +79,8 @@ typedef struct rae_config {
     int32_t neg_mode;         /* RAE_NEG_*                                                */
     int64_t neg_stride;       /* row stride (elements) of the neg arrays                  */
     int64_t index_window;     /* batches whose row index is held at once (0 = default)   */
+    int32_t mfma_bf16;        /* RESCAL / hybrid: bf16 MFMA operands for the R/C GEMMs    *
+                               * (fp32 accumulate; BASELINE config 5); 0 = exact fp32     */
 } rae_config;
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):

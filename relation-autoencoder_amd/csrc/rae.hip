@@ -51,10 +51,12 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
 __host__ __device__ inline int bil_m_tasks(int l, int r) {
     return ((l + 15) / 16) * (int)(((int64_t)r * r + 63) / 64);
 }
-template <bool V4>
+template <bool V4, bool BF16>
 __global__ __launch_bounds__(RAE_BT) void k_bil_m(StepArgs a) {
     const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
-    if (t < bil_m_tasks(a.l, a.r)) bil_gemm_m<V4>(a, t, threadIdx.x & 63);
+    if (t >= bil_m_tasks(a.l, a.r)) return;
+    if constexpr (BF16) bil_gemm_m_bf16(a, t, threadIdx.x & 63);
+    else bil_gemm_m<V4>(a, t, threadIdx.x & 63);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_bil_dec(StepArgs a) {
@@ -64,9 +66,12 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_dec(StepArgs a) {
 __host__ __device__ inline int bil_dp_tasks(int l, int m, int nib) {
     return ((l + 15) / 16) * ((m + 15) / 16) * nib;
 }
+template <bool BF16>
 __global__ __launch_bounds__(RAE_BT) void k_bil_dp(StepArgs a) {
     const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
-    if (t < bil_dp_tasks(a.l, a.m, a.nib)) bil_gemm_dp(a, t, threadIdx.x & 63);
+    if (t >= bil_dp_tasks(a.l, a.m, a.nib)) return;
+    if constexpr (BF16) bil_gemm_dp_bf16(a, t, threadIdx.x & 63);
+    else bil_gemm_dp(a, t, threadIdx.x & 63);
 }
 __global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
     __shared__ float sdp[1024];
@@ -411,6 +416,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     const bool bil = c.decoder != RAE_DEC_SP;
     a.nib = bil ? (c.embed + RAE_IB - 1) / RAE_IB : 0;
+    a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
     const size_t o_mbuf = bil ? take(4ull * c.batch_size * c.embed * c.embed) : 0;
     const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
@@ -525,10 +531,16 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
     hipLaunchKernelGGL((k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
     const int gm = ceil_div(bil_m_tasks(a.l, a.r), RAE_NWAVE);
-    hipLaunchKernelGGL((k_bil_m<V4>), dim3(gm), dim3(RAE_BT), 0, st, a);
+    if (V4 && a.bf16)
+        hipLaunchKernelGGL((k_bil_m<V4, true>), dim3(gm), dim3(RAE_BT), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
     hipLaunchKernelGGL((k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
-    hipLaunchKernelGGL(k_bil_dp, dim3(gd), dim3(RAE_BT), 0, st, a);
+    if (a.bf16)
+        hipLaunchKernelGGL(k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
     hipLaunchKernelGGL(k_bil_fin, ge, dim3(RAE_BT), 0, st, a);
 }
 

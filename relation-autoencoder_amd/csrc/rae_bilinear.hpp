@@ -137,6 +137,121 @@ __device__ void bil_gemm_m(const StepArgs& a, int t, int lane) {
     }
 }
 
+// ---- bf16-operand forms (rae_config.mfma_bf16; BASELINE config 5) ------------------------
+// v_mfma_f32_16x16x32_bf16: lane l holds A[l&15][8(l>>4) + e] and B[8(l>>4) + e][l&15],
+// e = 0..7; fp32 values are rounded to bf16 (v_cvt_pk_bf16_f32, nearest even) as they enter
+// the fragment, accumulation stays fp32.  K = 32 per instruction instead of 4.
+typedef __bf16 rae_bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
+    rae_bf16x8 v;
+    v[0] = (__bf16)lo.x; v[1] = (__bf16)lo.y; v[2] = (__bf16)lo.z; v[3] = (__bf16)lo.w;
+    v[4] = (__bf16)hi.x; v[5] = (__bf16)hi.y; v[6] = (__bf16)hi.z; v[7] = (__bf16)hi.w;
+    return v;
+}
+
+// M[b][ij] (as bil_gemm_m) with bf16 operands; m % 4 == 0
+__device__ void bil_gemm_m_bf16(const StepArgs& a, int t, int lane) {
+    const int l = a.l, m = a.m, r = a.r;
+    const int nbt = (l + 15) / 16;
+    const int64_t rr = (int64_t)r * r;
+    const int bt = t % nbt;
+    const int64_t ij0 = (int64_t)(t / nbt) * 64;
+    const int li = lane & 15, g = lane >> 4;
+    const int b = bt * 16 + li;
+    const bool bv = b < l;
+    const float* Prow = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec + a.lay.oP;
+    const float* Rrow[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t ij = ij0 + 16 * n + li;
+        Rrow[n] = a.R3 + (ij < rr ? ij : rr - 1) * m;
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    rae_bf4 acc[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < m; k0 += 32) {
+        const int ka = k0 + 8 * g, kb = ka + 4;
+        const bool va = ka < m, vb = kb < m;
+        float4 p0 = *reinterpret_cast<const float4*>(Prow + (va ? ka : 0));
+        float4 p1 = *reinterpret_cast<const float4*>(Prow + (vb ? kb : 0));
+        if (!va || !bv) p0 = z4;
+        if (!vb || !bv) p1 = z4;
+        const rae_bf16x8 pa = to_bf16x8(p0, p1);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            float4 r0 = *reinterpret_cast<const float4*>(Rrow[n] + (va ? ka : 0));
+            float4 r1 = *reinterpret_cast<const float4*>(Rrow[n] + (vb ? kb : 0));
+            if (!va) r0 = z4;
+            if (!vb) r1 = z4;
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, to_bf16x8(r0, r1), acc[n], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t ij = ij0 + 16 * n + li;
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int bo = bt * 16 + g * 4 + reg;
+            if (bo < l && ij < rr) a.Mbuf[(int64_t)bo * rr + ij] = acc[n][reg];
+        }
+    }
+}
+
+// dP partials (as bil_gemm_dp) with bf16 operands; K = j in steps of 32
+__device__ void bil_gemm_dp_bf16(const StepArgs& a, int t, int lane) {
+    const int l = a.l, m = a.m, r = a.r;
+    const int nbt = (l + 15) / 16, nkt = (m + 15) / 16;
+    const int bt = t % nbt, rest = t / nbt;
+    const int kt = rest % nkt, ib = rest / nkt;
+    const int li = lane & 15, g = lane >> 4;
+    const int b = bt * 16 + li;
+    const bool bv = b < l;
+    const float* er = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec;
+    const int k = kt * 16 + li;
+    const bool kv = k < m;
+    const int kc = kv ? k : 0;
+    const int i0 = ib * RAE_IB;
+    float xi[RAE_IB], ai[RAE_IB];
+#pragma unroll
+    for (int q = 0; q < RAE_IB; ++q) {
+        const int i = min(i0 + q, r - 1);
+        const bool use = bv && (i0 + q) < r;
+        xi[q] = use ? er[a.lay.oX + i] : 0.f;
+        ai[q] = use ? er[a.lay.oA1 + i] : 0.f;
+    }
+    rae_bf4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < r; j0 += 32) {
+        const int jb = j0 + 8 * g;
+        float a2j[8], yj[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bool jv = jb + e < r;
+            a2j[e] = jv ? er[a.lay.oA2 + jb + e] : 0.f;
+            yj[e] = jv ? er[a.lay.oY + jb + e] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < RAE_IB; ++q) {
+            const int i = min(i0 + q, r - 1);
+            rae_bf16x8 ua, rb;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int j = jb + e;
+                const bool jv = j < r;
+                ua[e] = (__bf16)(xi[q] * a2j[e] + ai[q] * yj[e]);
+                rb[e] = (__bf16)((jv && kv) ? a.R3[((int64_t)i * r + (jv ? j : 0)) * m + kc] : 0.f);
+            }
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, rb, acc, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int bo = bt * 16 + g * 4 + reg;
+        if (bo < l && kv) a.dPpart[((int64_t)ib * l + bo) * m + k] = acc[reg];
+    }
+}
+
 // ---- k_bil_dec helpers ----------------------------------------------------------------------
 struct BilSmem {
     float *v, *w, *a1, *a2, *wC1, *wC2, *x, *y, *My, *Mtx, *dw1, *dw2, *rows, *part, *dots, *Abv,
@@ -467,6 +582,44 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
 // ---- update: 16 rows ij of the R/C tensor (viewed as (r*r, m)) against all m columns ------
 // gR[ij][k] = sum_b U_b[ij] P_b[k] over the global batch, then the optimizer in place.
 // A[ij][kk] = U_{b0+kk}[ij], B[kk][k] = P_{b0+kk}[k], D[ij][k].
+// bf16-operand gradient of 16 rows ij x 16 columns per tile: K = examples in steps of 32
+__device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ijt, int kg0, int nk,
+                                                       rae_bf4* acc, int lane) {
+    const int m = a.m, r = a.r, L = a.L;
+    const int64_t rr = (int64_t)r * r;
+    const int li = lane & 15, g = lane >> 4;
+    const int64_t ij = (int64_t)ijt * 16 + li;
+    const bool ijv = ij < rr;
+    const int ijc = (int)(ijv ? ij : 0);
+    const int i = ijc / r, j = ijc - (ijc / r) * r;
+    for (int b0 = 0; b0 < L; b0 += 32) {
+        rae_bf16x8 ua;
+        const float* erb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int b = b0 + 8 * g + e;
+            const bool bv = b < L;
+            const float* er = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec;
+            erb[e] = er;
+            const float u = er[a.lay.oX + i] * er[a.lay.oA2 + j] + er[a.lay.oA1 + i] * er[a.lay.oY + j];
+            ua[e] = (__bf16)((bv && ijv) ? u : 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < RAE_KG; ++q) {
+            if (q >= nk) continue;
+            const int k = (kg0 + q) * 16 + li;
+            const bool kv = k < m;
+            rae_bf16x8 pb;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const bool bv = b0 + 8 * g + e < L;
+                pb[e] = (__bf16)((bv && kv) ? erb[e][a.lay.oP + (kv ? k : 0)] : 0.f);
+            }
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, pb, acc[q], 0, 0, 0);
+        }
+    }
+}
+
 template <int OPT>
 __device__ void task_bilinear_rows(const StepArgs& a, int ijt, int slot, int lane) {
     const int m = a.m, r = a.r, L = a.L;
@@ -484,7 +637,8 @@ __device__ void task_bilinear_rows(const StepArgs& a, int ijt, int slot, int lan
         rae_bf4 acc[RAE_KG];
 #pragma unroll
         for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-        for (int b0 = 0; b0 < L; b0 += 4) {
+        if (a.bf16) bilinear_rows_acc_bf16(a, ijt, kg0, nk, acc, lane);
+        else for (int b0 = 0; b0 < L; b0 += 4) {
             const int b = b0 + kk;
             const bool bv = b < L;
             const float* er = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec;

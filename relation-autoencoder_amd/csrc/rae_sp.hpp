@@ -576,6 +576,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
         }
     }
     __syncthreads();
+    RAE_STAMP(a, 8);
 
     // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
     sp_weighted_rows<V4>(Dm, S);
@@ -583,6 +584,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     __syncthreads();
     RAE_STAMP(a, 5);
     sp_project_back<V4>(a, Dm, S, cc_);
+    RAE_STAMP(a, 9);
     softmax_backward(a, Dm, S);
     RAE_STAMP(a, 6);
     write_record(a, Dm, S, a.ex + (int64_t)bg * a.lay.rec);

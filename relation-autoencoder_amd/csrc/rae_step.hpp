@@ -88,6 +88,7 @@ struct StepArgs {
     float* Mbuf;         // bilinear: M_b = sum_k P_bk R[:,:,k] of this rank's examples (l, r*r)
     float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
     int nib;             // bilinear: number of i-blocks of the dP contraction
+    int bf16;            // bilinear: bf16 MFMA operands (fp32 accumulation) for the R GEMMs
     double* regpart;     // [nreg][2] L1/L2 partials of regularised rows
     int nregC;           // number of decoder-row partial slots
     int nregW;           // number of dense-W block partial slots

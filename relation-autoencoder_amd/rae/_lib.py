@@ -37,7 +37,7 @@ class RaeConfig(C.Structure):
         ("learning_rate", C.c_float), ("alpha", C.c_float), ("lambda1", C.c_float),
         ("lambda2", C.c_float), ("ext_reg", C.c_int32), ("max_batch_nnz", C.c_int32),
         ("max_row_nnz", C.c_int32), ("neg_mode", C.c_int32), ("neg_stride", C.c_int64),
-        ("index_window", C.c_int64),
+        ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
     ]
 
 

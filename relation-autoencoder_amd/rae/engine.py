@@ -46,7 +46,7 @@ class DeviceSplit:
 class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
-                 index_window=0, device=None):
+                 index_window=0, device=None, mfma_bf16=False):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -88,6 +88,7 @@ class TrainEngine:
         cfg.neg_mode = _lib.RAE_NEG_PER_EPOCH
         cfg.neg_stride = self.N
         cfg.index_window = int(index_window)
+        cfg.mfma_bf16 = 1 if mfma_bf16 else 0
         self.cfg = cfg
         self.rec_floats = int(self.lib.rae_exchange_record_floats(C.byref(cfg)))
         self.exchange_buf = torch.zeros(int(self.lib.rae_exchange_floats(C.byref(cfg))),

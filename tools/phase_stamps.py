@@ -109,6 +109,11 @@ def main():
         print(f"  {kind:8s}: " + "  ".join(f"{c} {np.median(per[:, i]):.2f}/{per[:, i].max():.2f}"
                                            for i, c in enumerate(cols)))
     print(f"  forward span (first start -> last stamp): median {np.median(spans):.2f} us")
+    sub = np.concatenate([f[HA + HW:gf] for f in fw])
+    if np.all(sub[:, 8] > 0):
+        print(f"  sub-phases: coef {np.median(sub[:, 8] - sub[:, 4]):.2f}  weighted-rows "
+              f"{np.median(sub[:, 5] - sub[:, 8]):.2f}  C^T.dw {np.median(sub[:, 9] - sub[:, 5]):.2f}"
+              f"  softmax-bwd {np.median(sub[:, 6] - sub[:, 9]):.2f}")
     clk = []
     for f in fw:
         ex = f[HA + HW:gf]
