@@ -30,6 +30,9 @@
 using namespace rae;
 
 #define RAE_VERSION 1
+#ifndef RAE_UPD_WPE
+#define RAE_UPD_WPE 6   // SP update: <= 85 VGPRs -> 24 waves per CU, a C3 step's row tasks all resident
+#endif
 
 // ======================================================================================
 // kernels
@@ -39,7 +42,8 @@ __global__ __launch_bounds__(RAE_FBT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = *a.cursor + a.step_offset;
-    sp_example<V4, D>(a, g, blockIdx.x, smem);
+    if constexpr (D::fixed && V4) sp_example_fast<D>(a, g, blockIdx.x, smem);
+    else sp_example<V4, D>(a, g, blockIdx.x, smem);
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
@@ -110,7 +114,7 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 #endif
 
 template <int OPT, bool V4, int Q, bool BIL>
-__global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
+__device__ __forceinline__ void update_body(const StepArgs& a) {
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
     const int nw = gridDim.x * RAE_NWAVE;
@@ -139,6 +143,9 @@ __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
             }
         }
 #endif
+#ifdef RAE_SKIP_TILES
+        if (tt < nCt + nRt + mt + 1) continue;     // diagnostic: row tasks alone
+#endif
         if (tt < nCt) {
             const int which = tt / (rt * mt), ti = tt - which * rt * mt;
             task_mfma_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
@@ -166,6 +173,9 @@ __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
             continue;
         }
         tt -= 1;
+#ifdef RAE_SKIP_ROWS
+        if (true) continue;     // diagnostic: tile tasks alone
+#endif
         if (tt < TA) {
             task_entity_row<OPT, V4, Q, BIL>(a, slot, tt, TA, CA, lane);
             RAE_WAVE_END();
@@ -177,6 +187,21 @@ __global__ __launch_bounds__(RAE_BT) void k_update(StepArgs a) {
         if (a.stamps && lane == 0 && t == gw) a.stamps[(size_t)gw * 4 + 2] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
+}
+
+// SP and bilinear variants (the bilinear R-row tasks need more registers).
+#if RAE_UPD_WPE > 0
+#define RAE_UPD_ATTR __attribute__((amdgpu_waves_per_eu(RAE_UPD_WPE, RAE_UPD_WPE)))
+#else
+#define RAE_UPD_ATTR
+#endif
+template <int OPT, bool V4, int Q>
+__global__ __launch_bounds__(RAE_BT) RAE_UPD_ATTR void k_update(StepArgs a) {
+    update_body<OPT, V4, Q, false>(a);
+}
+template <int OPT, bool V4, int Q>
+__global__ __launch_bounds__(RAE_BT) void k_update_bil(StepArgs a) {
+    update_body<OPT, V4, Q, true>(a);
 }
 
 // Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,
@@ -559,8 +584,13 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
 
 template <int OPT, bool V4, bool BIL>
 static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
-    if (p->q == 1) hipLaunchKernelGGL((k_update<OPT, V4, 1, BIL>), gu, bt, 0, st, a);
-    else hipLaunchKernelGGL((k_update<OPT, V4, 2, BIL>), gu, bt, 0, st, a);
+    if constexpr (BIL) {
+        if (p->q == 1) hipLaunchKernelGGL((k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
+        else hipLaunchKernelGGL((k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
+    } else {
+        if (p->q == 1) hipLaunchKernelGGL((k_update<OPT, V4, 1>), gu, bt, 0, st, a);
+        else hipLaunchKernelGGL((k_update<OPT, V4, 2>), gu, bt, 0, st, a);
+    }
 }
 template <int OPT, bool V4>
 static void launch_update_v(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {

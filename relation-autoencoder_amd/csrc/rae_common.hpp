@@ -134,6 +134,31 @@ __device__ __forceinline__ float sigmoid(float x) {
     return z / (1.f + z);
 }
 
+// One exp shared by sigmoid(x) and softplus(x) = log(1 + e^x), hardware transcendental
+// forms (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): e = exp(-|x|),
+//   sigmoid(x)  = x >= 0 ? 1/(1+e) : e/(1+e)
+//   softplus(x) = max(x, 0) + log(1 + e)      (log_sigmoid(x) = -softplus(-x))
+__device__ __forceinline__ void sigmoid_softplus(float x, float& sig, float& sp) {
+    const float e = __expf(-fabsf(x));
+    const float r = __builtin_amdgcn_rcpf(1.f + e);
+    sig = x >= 0.f ? r : e * r;
+    sp = fmaxf(x, 0.f) + __logf(1.f + e);
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() carries a workgroup fence,
+// for which the compiler drains vmcnt -- every global load and LDS-DMA the wave has in
+// flight -- before the s_barrier.  Where a wave keeps bulk loads in flight across a
+// barrier (decoder matrices, A-row DMA) that would put them on the critical path; this
+// waits only for the wave's own LDS (and scalar) traffic.  Data a wave brought in by
+// LDS-DMA becomes visible to the others only after that wave's s_waitcnt vmcnt(0) and a
+// following barrier (dma_visible_barrier).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void dma_visible_barrier() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // learning/Optimizers.py:30-31  acc <- acc + g^2 ; p <- p - lr*g/(sqrt(acc)+1e-6)
 // learning/Optimizers.py:51     p <- p - lr*g                         (SGD)
 template <int OPT>

@@ -29,6 +29,9 @@ namespace rae {
 
 #define RAE_FNW (RAE_FBT / RAE_WAVE)     // waves per forward workgroup
 #define RAE_NG (RAE_FBT / 16)            // 16-lane groups per forward workgroup
+#ifndef RAE_CEARLY
+#define RAE_CEARLY 0   // measured: C loads first delay the id chain (vmcnt is in order)
+#endif
 
 // ---- compile-time or runtime shapes ------------------------------------------------------
 struct DynDims {
@@ -132,12 +135,13 @@ typedef __attribute__((address_space(1))) void rae_glob_void;
 
 template <bool V4, class D>
 __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, const D& Dm, ExampleSmem& S,
-                                                int NR, int skip_e2) {
+                                                int NR, int skip_e2, int w0 = 0,
+                                                int nw = RAE_FNW) {
     constexpr int VW = V4 ? 4 : 1;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) - w0;
     const int rv = Dm.r / VW, r4 = align4(Dm.r);
     const int nchunk = (rv + 63) / 64;
-    for (int t = w; t < NR * nchunk; t += RAE_FNW) {
+    for (int t = w; t < NR * nchunk; t += nw) {
         const int rho = t / nchunk, ch = t - rho * nchunk;
         const int j = (rho == 0) ? 0 : rho + skip_e2;
         const int c = ch * 64 + lane;
@@ -180,8 +184,13 @@ struct CCache {
 #pragma unroll
             for (int cc = 0; cc < CC; ++cc) {
                 const int c = min(c0 + q + 16 * cc, mv - 1);
+#ifdef RAE_SKIP_C
+                vzero(c1[ra][cc]);     // diagnostic: no decoder-matrix traffic
+                vzero(c2[ra][cc]);
+#else
                 c1[ra][cc] = C1v[i * mv + c];
                 c2[ra][cc] = C2v[i * mv + c];
+#endif
             }
         }
     }
@@ -501,13 +510,21 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 #endif
+    CCache<V4, D> cc_;
+#if RAE_CEARLY
+    // the decoder matrices do not depend on the batch: their loads go out first and land
+    // while the id -> feature -> W-row chain runs
+    if (CCache<V4, D>::FITS) cc_.load(a, Dm, 0, 0);
+    constexpr bool kLoadC = false;
+#else
+    constexpr bool kLoadC = CCache<V4, D>::FITS;
+#endif
     load_ids(a, Dm, ex, col, S);
     __syncthreads();
     RAE_STAMP(a, 1);
     const int NJ = 2 + 2 * s;
     if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
-    CCache<V4, D> cc_;
-    encoder_forward<V4, V4, CCache<V4, D>::FITS>(a, Dm, S, NR, 1, cc_);
+    encoder_forward<V4, V4, kLoadC>(a, Dm, S, NR, 1, cc_);
     const float H = S.sred[40];
     RAE_STAMP(a, 2);
     sp_project<V4>(a, Dm, S, cc_);
@@ -544,6 +561,11 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 4);
 
     // scores, loss, coefficients (wave 0)
+#ifdef RAE_ICACHE_TEST
+#pragma clang loop unroll(disable)
+    for (int rep = 0; rep < 2; ++rep) {
+    if (rep == 1) RAE_STAMP(a, 10);
+#endif
     if (w == 0) {
         const float left = S.sdots[0], right = S.sdots[1];
         float sdg1 = 0.f, sdg2 = 0.f, sls = 0.f;
@@ -576,6 +598,10 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
         }
     }
     __syncthreads();
+#ifdef RAE_ICACHE_TEST
+    if (rep == 1) RAE_STAMP(a, 11);
+    }
+#endif
     RAE_STAMP(a, 8);
 
     // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
@@ -593,5 +619,350 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
 #endif
 }
+
+// ---- the SP example path for compile-time shapes (BASELINE configs) ---------------------
+// Same arithmetic as sp_example, re-timed for a 100-example step where the kernel is a
+// dependent chain: waves 0-3 run the critical chain (ids -> feature ids -> W rows -> S ->
+// softmax) while waves 4-7 issue the A-row LDS-DMA and the Ab loads, and every wave
+// then issues its share of the decoder-matrix loads.  No barrier drains vmcnt until the
+// decoder matrices are needed (lds_barrier), so the ~200 KB of bulk loads per CU overlap
+// the chain instead of sitting in front of it.  Softmax and the score coefficients use
+// hardware exp/log/rcp; the coefficient work is spread over 2s lanes.
+template <class D>
+__device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem) {
+    static_assert(D::fixed && D::m % 4 == 0 && D::r % 4 == 0 && D::s <= 32, "fast SP path");
+    constexpr int m = D::m, r = D::r, s = D::s, NR = 1 + 2 * s, NJ = 2 + 2 * s;
+    constexpr int MV = m / 4, NSL = 256 / MV, KF = 3;
+    constexpr int r4 = r, mp = ((m + 255) / 256) * 256;
+    const D Dm(a);
+    // wave index as a scalar: role branches are then uniform control flow (s_cbranch on an
+    // SGPR), not exec-masked linearised code whose register reuse forces vmcnt(0) waits
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
+    const int bg = a.rank * a.l + bl;
+    const int64_t ex = g * (int64_t)a.L + bg;
+    const int64_t col = a.neg_mode ? ex : (int64_t)bg;
+
+    RAE_STAMP(a, 0);
+#ifdef RAE_STAMPS
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
+#endif
+    load_ids(a, Dm, ex, col, S);
+    constexpr int NI = mp / RAE_WAVE;
+    float wbk[NI];                           // wave 0: the bias entries it reduces
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        wbk[i] = (w == 0 && k < m) ? a.Wb[k] : 0.f;
+    }
+    if (tid == 0) S.sint[4] = 0;             // arrival counter of the W-row waves
+    lds_barrier();
+    RAE_STAMP(a, 1);
+    const int p0 = S.sint[0], nf = S.sint[1] - p0;
+    if (nf > 256) {                          // long feature rows: the general path
+        lds_barrier();
+        sp_example<true, D>(a, g, bl, smem);
+        return;
+    }
+    if (w < 4 && tid < nf) {
+        S.sfidx[tid] = a.indices[p0 + tid];
+        S.sfval[tid] = a.values ? a.values[p0 + tid] : 1.f;
+    }
+    lds_barrier();
+    RAE_STAMP(a, 10);
+
+    // Per-CU issue order W rows -> A rows -> decoder matrices: vmcnt and the CU's memory
+    // queue are in issue order, so the 5 KB of W rows the chain waits on go out first, the
+    // A rows (needed after C.P) next, and the 160 KB of decoder matrices last.
+    // W rows (waves 0-3): slot = feature lane group, c = float4 column.
+    const float4* W4 = reinterpret_cast<const float4*>(a.W);
+    const int slot = tid / MV, c = tid - slot * MV;
+    float4 wv[KF];
+    float fv[KF];
+    if (w < 4) {
+#pragma unroll
+        for (int k = 0; k < KF; ++k) {
+            const int f = slot + NSL * k;
+            const bool ok = slot < NSL && f < nf;
+            const int fi = S.sfidx[f < 256 ? f : 255];
+            wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
+            fv[k] = ok ? S.sfval[f < 256 ? f : 255] : 0.f;
+        }
+    }
+    lds_barrier();                           // every W-row load is issued
+    RAE_STAMP(a, 11);
+    // Each role is one uniform branch, so the compiler's vmcnt bookkeeping for the W-row
+    // FMAs sees only the 28 decoder-matrix loads behind them (not the DMA loop).
+    float abv = 0.f;
+    CCache<true, D> cc_;
+    if (w < 4) {
+        asm volatile("" ::: "memory");
+        cc_.load(a, Dm, 0, 0);
+        float4 acc;
+        vzero(acc);
+#pragma unroll
+        for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
+        if (slot < NSL) {
+            for (int f = slot + NSL * KF; f < nf; f += NSL)      // rows with > NSL*KF features
+                vfma(acc, S.sfval[f], W4[(int64_t)S.sfidx[f] * MV + c]);
+            reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
+        }
+    } else {
+        gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
+        if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
+        asm volatile("" ::: "memory");
+        cc_.load(a, Dm, 0, 0);
+    }
+    RAE_STAMP(a, 12);
+    // S = X.W + Wb and the softmax run in wave 0 as soon as waves 0-3 have their partial
+    // sums in LDS (LDS arrival counter) -- not behind a block barrier, which would also
+    // wait for waves 4-7, still issuing (and back-pressured on) the bulk loads.
+    if (w < 4) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&S.sint[4], 1);
+    }
+    if (w == 0) {
+        while (__hip_atomic_load(&S.sint[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
+            __builtin_amdgcn_s_sleep(1);
+        RAE_STAMP(a, 13);
+        float sv[NI];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            float v = 0.f;
+            if (k < m) {
+#pragma unroll
+                for (int sl = 0; sl < NSL; ++sl) v += S.spart[sl * m + k];
+                v += wbk[i];
+                mx = fmaxf(mx, v);
+            }
+            sv[i] = v;
+        }
+        mx = wave_max(mx);
+        float ev[NI];
+        float se = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            ev[i] = k < m ? __expf(sv[i] - mx) : 0.f;
+            se += ev[i];
+        }
+        se = wave_sum(se);
+        const float inv = 1.f / se, lse = __logf(se);
+        float hp = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            const float z = k < m ? sv[i] - mx : 0.f;
+            const float p = ev[i] * inv;
+            S.sZ[k] = z;
+            S.sP[k] = p;
+            hp += p * (z - lse);
+        }
+        hp = wave_sum(hp);
+        if (lane == 0) S.sred[40] = -a.alpha * hp;
+    }
+    lds_barrier();
+    const float H = S.sred[40];
+    RAE_STAMP(a, 2);
+    sp_project<true>(a, Dm, S, cc_);
+    if (w >= 4 && tid - 256 < NJ) S.sAbv[tid - 256] = abv;
+    dma_visible_barrier();                   // A rows (LDS-DMA) and Ab landed
+    RAE_STAMP(a, 3);
+
+    // dot products: wave w takes rows w, w+8, ...; all LDS reads first, then the
+    // independent wave reductions interleave
+    constexpr int RV = r / 4;
+    static_assert(RV <= RAE_WAVE, "one float4 column per lane");
+    const bool lv = lane < RV;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* Rv = reinterpret_cast<const float4*>(S.srows);
+    const float4 wc1 = lv ? reinterpret_cast<const float4*>(S.swC1)[lane] : z4;
+    const float4 wc2 = lv ? reinterpret_cast<const float4*>(S.swC2)[lane] : z4;
+    {
+        constexpr int RPW = (NR + RAE_FNW - 1) / RAE_FNW;
+        float d[RPW];
+        float d0b = 0.f;
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int rho = w + RAE_FNW * q;
+            float v = 0.f;
+            if (rho < NR && lv) {
+                const float4 x = Rv[rho * RV + lane];
+                v = vdot(x, rho > s ? wc2 : wc1);          // rows 1..s: neg1, s+1..2s: neg2
+                if (rho == 0) d0b = vdot(x, wc2);
+            }
+            d[q] = v;
+        }
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) d[q] = wave_sum(d[q]);
+        if (w == 0) d0b = wave_sum(d0b);
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < RPW; ++q) {
+                const int rho = w + RAE_FNW * q;
+                if (rho == 0) {
+                    S.sdots[0] = d[q];       // left  = <wC1, A[e1]>
+                    S.sdots[1] = d0b;        // right = <wC2, A[e1]>
+                } else if (rho < NR) {
+                    S.sdots[rho + 1] = d[q];
+                }
+            }
+        }
+    }
+    lds_barrier();
+    RAE_STAMP(a, 4);
+
+    // scores, loss and coefficients -- computed by EVERY wave (identical values; no barrier
+    // to broadcast them): lanes 0..s-1 neg1[t], lanes 32..32+s-1 neg2[t]
+    const float left = S.sdots[0], right = S.sdots[1];
+    const int tq = lane & 31;
+    const bool hi = lane >= 32;
+    float dg = 0.f, ls = 0.f;
+    if (tq < s) {
+        const int j = 2 + (hi ? s : 0) + tq;
+        const float gg = S.sdots[j] + (hi ? left : right) + S.sAbv[j];
+        float sg, spl;
+        sigmoid_softplus(gg, sg, spl);
+        dg = sg * a.invD;
+        ls = -spl;                           // log_sigmoid(-g)
+    }
+    float hs = group16_sum(dg);
+    hs += __uint_as_float(xor16_u32(__float_as_uint(hs)));
+    const float other = __uint_as_float(xor32_u32(__float_as_uint(hs)));
+    const float sdg1 = hi ? other : hs, sdg2 = hi ? hs : other;
+    const float one = left + right;
+    const float u1 = one + S.sAbv[0], u2 = one + S.sAbv[1];
+    float su1, spu1, su2, spu2;
+    sigmoid_softplus(-u1, su1, spu1);
+    sigmoid_softplus(-u2, su2, spu2);
+    const float du1 = -su1 * a.invD, du2 = -su2 * a.invD;
+    const float dl = du1 + du2 + sdg2;       // d cost / d left
+    const float dr = du1 + du2 + sdg1;       // d cost / d right
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+
+    // dw1 = dl a1 + sum_t dg1_t n1_t (wave 0), dw2 = dr a1 + sum_t dg2_t n2_t (wave 1):
+    // one float4 column per lane, the t-sum in order, coefficients broadcast by readlane
+    if (w < 2) {
+        const float c0 = w == 0 ? dl : dr;
+        float4 v = z4;
+        if (lv) {
+            vfma(v, c0, Rv[lane]);
+#pragma unroll
+            for (int t = 0; t < s; ++t) {
+                const float ct = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg),
+                                                                           (w == 0 ? 0 : 32) + t));
+                vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lane]);
+            }
+            reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
+            reinterpret_cast<float4*>(rec + (w == 0 ? a.lay.odw1 : a.lay.odw2))[lane] = v;
+        }
+    } else if (w == 2) {                     // V1 = wC1, V2 = wC2
+        if (lv) {
+            reinterpret_cast<float4*>(rec + a.lay.oV1)[lane] = wc1;
+            reinterpret_cast<float4*>(rec + a.lay.oV2)[lane] = wc2;
+        }
+    } else if (w == 3) {                     // G1 = dl wC1 + dr wC2 (A[e1]'s gradient)
+        if (lv) {
+            float4 gv;
+            gv.x = dl * wc1.x + dr * wc2.x;
+            gv.y = dl * wc1.y + dr * wc2.y;
+            gv.z = dl * wc1.z + dr * wc2.z;
+            gv.w = dl * wc1.w + dr * wc2.w;
+            reinterpret_cast<float4*>(rec + a.lay.oG1)[lane] = gv;
+        }
+    } else if (w == 4) {                     // coefficients (c_j, gamma_j) and the loss
+        if (tq < s) {
+            const int j = 2 + (hi ? s : 0) + tq;
+            rec[a.lay.ocoef + 2 * j] = dg;
+            rec[a.lay.ocoef + 2 * j + 1] = dg;
+        }
+        const float sls = wave_sum(ls);
+        if (lane == 0) {
+            rec[a.lay.ocoef + 0] = 1.f;
+            rec[a.lay.ocoef + 1] = du1;
+            rec[a.lay.ocoef + 2] = 0.f;
+            rec[a.lay.ocoef + 3] = du2;
+            rec[a.lay.oloss] = -spu1 - spu2 + 2.f * H + sls;
+        }
+    }
+    lds_barrier();
+    RAE_STAMP(a, 8);
+    RAE_STAMP(a, 5);
+
+    // dP = C1^T dw1 + C2^T dw2: per-wave partials (rows held in registers), reduced over the
+    // wave's 4 lane groups; the 8 wave partials are summed by wave 0 below
+    {
+        typedef CCache<true, D> CC_;
+        const int gid = tid >> 4, q = tid & 15;
+        float4 acc[CC_::CC];
+#pragma unroll
+        for (int cc = 0; cc < CC_::CC; ++cc) acc[cc] = z4;
+#pragma unroll
+        for (int ra = 0; ra < CC_::RA; ++ra) {
+            const int i = gid + RAE_NG * ra;
+            const float d1 = i < r ? S.sdw1[i] : 0.f;
+            const float d2 = i < r ? S.sdw2[i] : 0.f;
+#pragma unroll
+            for (int cc = 0; cc < CC_::CC; ++cc) {
+                vfma(acc[cc], d1, cc_.c1[ra][cc]);
+                vfma(acc[cc], d2, cc_.c2[ra][cc]);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < CC_::CC; ++cc) {
+            float* v = reinterpret_cast<float*>(&acc[cc]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] += __uint_as_float(xor16_u32(__float_as_uint(v[e])));
+                v[e] += __uint_as_float(xor32_u32(__float_as_uint(v[e])));
+            }
+            const int col = q + 16 * cc;
+            if (lane < 16 && col < MV) reinterpret_cast<float4*>(S.spart + w * mp)[col] = acc[cc];
+        }
+    }
+    lds_barrier();
+    RAE_STAMP(a, 9);
+
+    // softmax backward (wave 0) straight into the record:
+    //   dS_k = P_k ((dP_k - sum_j P_j dP_j) + ce (z_k - sum_j P_j z_j))   (softmax_backward)
+    if (w == 0) {
+        const float ce = 2.f * a.alpha * a.invD;
+        float pk[NI], zk[NI], dp[NI];
+        float sd = 0.f, sz = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            float v = 0.f;
+            if (k < m) {
+#pragma unroll
+                for (int ww = 0; ww < RAE_FNW; ++ww) v += S.spart[ww * mp + k];
+            }
+            dp[i] = v;
+            pk[i] = k < m ? S.sP[k] : 0.f;
+            zk[i] = k < m ? S.sZ[k] : 0.f;
+            sd += pk[i] * dp[i];
+            sz += pk[i] * zk[i];
+        }
+        sd = wave_sum(sd);
+        sz = wave_sum(sz);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            if (k < m) {
+                rec[a.lay.oP + k] = pk[i];
+                rec[a.lay.odS + k] = pk[i] * ((dp[i] - sd) + ce * (zk[i] - sz));
+            }
+        }
+    }
+    RAE_STAMP(a, 6);
+    RAE_STAMP(a, 7);
+#ifdef RAE_STAMPS
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
+#endif
+}
+
 
 }  // namespace rae

@@ -29,7 +29,12 @@ namespace rae {
 //   D[row][col]            col = lane&15, row = (lane>>4)*4 + reg
 // SP/hybrid C1, C2: coef(b, i) = dw1_b[i] / dw2_b[i]; Wb (ones): one row of ones times dS_b.
 typedef float rae_f4 __attribute__((ext_vector_type(4)));
-#define RAE_TU 32    // k-steps (x4 examples) whose operands are loaded before the MFMA chain
+#ifndef RAE_TU
+#define RAE_TU 8     // k-steps (x4 examples) whose operands are loaded before the MFMA chain
+#ifndef RAE_UNR1
+#define RAE_UNR1 4
+#endif
+#endif
 
 template <int OPT>
 __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw,
@@ -40,37 +45,66 @@ __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows
     const bool iv = i < nrows, kv = k < m;
     const int ic = iv ? i : 0, kc = kv ? k : 0;
     rae_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#ifdef RAE_ICACHE_TEST
+#pragma clang loop unroll(disable)
+    for (int rep = 0; rep < 2; ++rep) {
+    if (rep == 1) {
+        if (a.stamps && lane == 0) {
+            const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+            if (slot == gw) a.stamps[(size_t)gw * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+        }
+        acc = rae_f4{0.f, 0.f, 0.f, 0.f};
+    }
+#endif
+    const int ox = odw + ic, oy = (ones ? a.lay.odS : a.lay.oP) + kc;   // Wb: sum_b dS_b
+    // the tile's parameters and accumulators are loaded up front, in flight with the records
+    const int col = k0 + li;
+    float pw[4], pa[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = i0 + lk * 4 + reg;
+        const bool ok = row < nrows && col < m && (!ones || row == i0);
+        const int o = ok ? (ones ? col : row * m + col) : 0;
+        pw[reg] = M[o];
+        pa[reg] = (OPT == 0) ? aM[o] : 0.f;
+    }
     for (int b0 = 0; b0 < L; b0 += 4 * RAE_TU) {
         float av[RAE_TU], bv[RAE_TU];
+        // every operand load goes out before the first MFMA: the sched_barrier keeps the
+        // scheduler from sinking each load next to its MFMA (which serialised 32 round trips)
 #pragma unroll
         for (int u = 0; u < RAE_TU; ++u) {
             const int b = b0 + 4 * u + lk;
-            const bool bvld = b < L;
-            const float* er = a.ex + (int64_t)(bvld ? b : 0) * a.lay.rec;
-            const float x = ones ? 1.f : er[odw + ic];
-            const float y = er[(ones ? a.lay.odS : a.lay.oP) + kc];   // Wb: sum_b dS_b
-            av[u] = (bvld && iv && (!ones || li == 0)) ? x : 0.f;
-            bv[u] = (bvld && kv) ? y : 0.f;
+            const int rb = (b < L ? b : 0) * a.lay.rec;
+            av[u] = ones ? 1.f : a.ex[rb + ox];
+            bv[u] = a.ex[rb + oy];
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < RAE_TU; ++u)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+        for (int u = 0; u < RAE_TU; ++u) {
+            const bool bvld = b0 + 4 * u + lk < L;
+            const float x = (bvld && iv && (!ones || li == 0)) ? av[u] : 0.f;
+            const float y = (bvld && kv) ? bv[u] : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, acc, 0, 0, 0);
+        }
     }
-    const int col = k0 + li;
+#ifdef RAE_ICACHE_TEST
+    }
+#endif
     float l1 = 0.f, l2 = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
         const int row = i0 + lk * 4 + reg;
         if (row < nrows && col < m && (!ones || row == i0)) {
-            const int64_t o = ones ? col : (int64_t)row * m + col;
-            const float w = M[o];
+            const int o = ones ? col : row * m + col;
+            const float w = pw[reg];
             float g = acc[reg];
             if (!ones && a.reg_on && a.ext_reg) {
                 g += a.l1adj * sgnf(w) + 2.f * a.l2adj * w;
                 l1 += fabsf(w);
                 l2 += w * w;
             }
-            float ac = (OPT == 0) ? aM[o] : 0.f;
+            float ac = pa[reg];
             M[o] = opt_update<OPT>(w, &ac, g, a.lr);
             if (OPT == 0) aM[o] = ac;
         }
@@ -157,7 +191,7 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 template <int OPT, bool V4, int Q, bool XY>
 __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, int C, int lane) {
     constexpr int VW = V4 ? 4 : 1;
-    constexpr int UNR = Q == 1 ? 8 : 4;
+    constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
     typedef typename VecT<V4>::T VT;
     const int r = a.r, nv = r / VW, s = a.s, NJ = 2 + 2 * s;
     const int64_t base = slot * a.RA;
@@ -222,7 +256,7 @@ template <int OPT, bool V4, int Q>
 __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int u, int U,
                                  int C, int lane) {
     constexpr int VW = V4 ? 4 : 1;
-    constexpr int UNR = Q == 1 ? 8 : 4;
+    constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
     typedef typename VecT<V4>::T VT;
     const int m = a.m, nv = m / VW;
     const int64_t base = slot * a.RW;

@@ -19,15 +19,21 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "relation-autoencoder_amd")
 DIAG = os.path.join(PKG, "rae", "librae_hip_diag.so")
+VARIANT = os.environ.get("RAE_VARIANT", "")      # extra -D flags: a diagnostic A/B build
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 
 
 def build_diag():
+    global DIAG
     import __graft_entry__ as ge
+    if VARIANT:
+        tag = VARIANT.replace("-D", "").replace("=", "").replace(" ", "_")
+        DIAG = os.path.join(PKG, "rae", f"librae_hip_diag_{tag}.so")
     src = os.path.join(PKG, "csrc", "rae.hip")
     if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < max(os.path.getmtime(s) for s in ge._sources()):
-        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DRAE_STAMPS", src, "-o", DIAG], check=True)
+        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DRAE_STAMPS", *VARIANT.split(), src, "-o", DIAG],
+                       check=True)
 
 
 def main():
@@ -114,6 +120,13 @@ def main():
         print(f"  sub-phases: coef {np.median(sub[:, 8] - sub[:, 4]):.2f}  weighted-rows "
               f"{np.median(sub[:, 5] - sub[:, 8]):.2f}  C^T.dw {np.median(sub[:, 9] - sub[:, 5]):.2f}"
               f"  softmax-bwd {np.median(sub[:, 6] - sub[:, 9]):.2f}")
+    if np.all(sub[:, 13] > 0) and np.all(sub[:, 12] > 0):
+        print(f"  fast-path encoder: indices {np.median(sub[:, 10] - sub[:, 1]):.2f}  W-issue "
+              f"{np.median(sub[:, 11] - sub[:, 10]):.2f}  W-wait+FMA(wave0) {np.median(sub[:, 12] - sub[:, 11]):.2f}"
+              f"  barrier {np.median(sub[:, 13] - sub[:, 12]):.2f}  S+softmax {np.median(sub[:, 2] - sub[:, 13]):.2f}")
+    elif np.all(sub[:, 11] > 0):
+        print(f"  icache test: coef rep0 {np.median(sub[:, 10] - sub[:, 4]):.2f}  rep1 "
+              f"{np.median(sub[:, 11] - sub[:, 10]):.2f}")
     clk = []
     for f in fw:
         ex = f[HA + HW:gf]
@@ -138,6 +151,13 @@ def main():
         if d:
             print(f"    {nm:8s} n={len(d) // len(t0s):5d}  dur {np.median(d):.2f}/{np.max(d):.2f}"
                   f"  start {np.median(st_):.2f}/{np.max(st_):.2f}")
+    mids = []
+    for t0, t1, v in t0s:
+        sel = v[(v[:, 1] == 0) & (v[:, 3] > 0)]
+        mids += list(zip((sel[:, 3] - sel[:, 0]) / 100.0, (sel[:, 2] - sel[:, 3]) / 100.0))
+    if mids:
+        mids = np.array(mids)
+        print(f"  icache test C-tile: start->rep1 {np.median(mids[:, 0]):.2f}  rep1->end {np.median(mids[:, 1]):.2f}")
     print(f"  update span: median {np.median([(t1 - t0) / 100.0 for t0, t1, _ in t0s]):.2f} us")
 
 

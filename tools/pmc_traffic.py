@@ -31,7 +31,7 @@ def _group(name):
     base = n.split("<")[0]
     if base == "k_forward" or base in ("k_bil_enc", "k_bil_m", "k_bil_dec", "k_bil_dp", "k_bil_fin"):
         return "k_forward", base
-    if base in ("k_update", "k_dense_w", "k_finalize_cost"):
+    if base in ("k_update", "k_update_bil", "k_dense_w", "k_finalize_cost"):
         return "k_update", base
     return None, base
 
