@@ -31,7 +31,9 @@ sys.path.insert(0, os.path.join(ROOT, "relation-autoencoder_amd"))
 METRIC = "train examples/sec (fwd+bwd) K=100 d=200 neg=20 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_16x16x4_f32)
-MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+MFMA_BF16_PEAK_TFS = 2500.0
+TIMING = ("HIP events stamped by the kernels' own dispatch packets (hipExtLaunchKernelGGL via "
+          "rae_time_next) on the launch stream, eager launches of the steps after the timed region")  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 # BASELINE.json configs: N triples, feature dim, K, embed, neg, decoder
 CONFIGS = {
@@ -195,8 +197,10 @@ def main():
     costs = eng.costs[W:W + K].cpu().numpy()
     assert np.all(np.isfinite(costs)), "non-finite cost"
 
-    # ---- per-kernel durations with HIP events on the launch stream (eager launches of
-    # the same step sequence continuing the epoch)
+    # ---- per-kernel durations: eager launches of the same step sequence continuing the
+    # epoch, each phase launched through rae_time_next (hipExtLaunchKernelGGL), so the HIP
+    # events carry the kernels' own dispatch begin/end timestamps -- the span rocprofv3
+    # --kernel-trace reports -- on the stream the kernels run on
     lib, plan = eng.lib, eng.plan
     st = torch.cuda.current_stream()
     sp_ = C.c_void_p(st.cuda_stream)
@@ -204,20 +208,35 @@ def main():
     n_it = min(args.kernel_iters, nb - b0, eng.index_window)
     lib.rae_build_index(plan, b0, n_it, sp_)
     lib.rae_set_cursor(plan, b0, sp_)
-    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(n_it)]
-    for i, (e0, e1, e2, e3) in enumerate(evs):
-        e0.record(st)
-        lib.rae_step_forward(plan, i, sp_)
-        e1.record(st)
+
+    def _ev():
+        h = C.c_void_p()
+        assert lib.rae_event_create(C.byref(h)) == 0, lib.rae_last_error()
+        return h
+    fev = [(_ev(), _ev()) for _ in range(n_it)]
+    uev = [(_ev(), _ev()) for _ in range(n_it)]
+    xev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(n_it)]
+    for i in range(n_it):
+        assert lib.rae_time_next(plan, fev[i][0], fev[i][1]) == 0
+        assert lib.rae_step_forward(plan, i, sp_) == 0, lib.rae_last_error()
+        xev[i][0].record(st)
         if exchange is not None:
             exchange(eng.exchange_buf)
-        e2.record(st)
-        lib.rae_step_update(plan, i, sp_)
-        e3.record(st)
+        xev[i][1].record(st)
+        assert lib.rae_time_next(plan, uev[i][0], uev[i][1]) == 0
+        assert lib.rae_step_update(plan, i, sp_) == 0, lib.rae_last_error()
     torch.cuda.synchronize()
-    fwd_ms = np.array([a.elapsed_time(b) for a, b, _, _ in evs])
-    xch_ms = np.array([b.elapsed_time(c) for _, b, c, _ in evs])
-    upd_ms = np.array([c.elapsed_time(d) for _, _, c, d in evs])
+
+    def _ms(pair):
+        v = C.c_float()
+        assert lib.rae_event_elapsed_ms(pair[0], pair[1], C.byref(v)) == 0, lib.rae_last_error()
+        return v.value
+    fwd_ms = np.array([_ms(e) for e in fev])
+    upd_ms = np.array([_ms(e) for e in uev])
+    xch_ms = np.array([a.elapsed_time(b) for a, b in xev])
+    for e in fev + uev:
+        lib.rae_event_destroy(e[0])
+        lib.rae_event_destroy(e[1])
     fwd_us = float(np.mean(fwd_ms) * 1e3)
     upd_us = float(np.mean(upd_ms) * 1e3)
     dec = cfg["dec"]
@@ -240,7 +259,7 @@ def main():
                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                 "traffic": (traffic or {}).get(dom), "bytes_per_launch": kern[dom]["bytes_per_launch"],
                 "avg_launch_us": kern[dom]["avg_launch_us"],
-                "timing": "HIP events around eager launches on the launch stream",
+                "timing": TIMING,
                 "traffic_source": (traffic or {}).get("source")}
     else:
         fl = step_flops(L, l, cfg["m"], cfg["r"], dec)
@@ -249,7 +268,7 @@ def main():
         roof = {"kernel": "step (forward phase + k_update)", "bound": "mfma", "achieved": ach,
                 "peak": pk, "unit": "TFLOP/s", "frac": ach / pk,
                 "traffic": None, "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
-                "timing": "HIP events around eager launches on the launch stream"}
+                "timing": TIMING}
 
     # ---- labelling pass over the whole train split (func['label_train'] at full-split scale,
     # the encoder kernel K1 in inference mode): fixed weights, probs + labels

@@ -150,6 +150,17 @@ int rae_step_update(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
  * rae_set_negatives(PER_CALL) + index + forward + update for `batch_index`.            */
 int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,
                    const int32_t* neg2_dev, rae_stream_t stream);
+/* Kernel timing (bench / profiling; no reference counterpart).  Arms the NEXT
+ * rae_step_forward or rae_step_update call on this plan: its kernels are launched with
+ * hipExtLaunchKernelGGL so `start_event` takes the first kernel's dispatch-begin timestamp
+ * and `stop_event` the last kernel's end timestamp -- the execution span rocprofv3
+ * --kernel-trace reports, without event-packet overhead.  Not for graph capture.
+ * Events are hipEvent_t handles (rae_event_create makes them).                         */
+int rae_time_next(rae_plan* plan, void* start_event, void* stop_event);
+int rae_event_create(void** event_out);
+int rae_event_destroy(void* event);
+/* waits for stop_event, then *ms = hipEventElapsedTime(start_event, stop_event) */
+int rae_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
 /* Device error word (overflow flags); host reads it with rae_check(). */
 int rae_check(rae_plan* plan);
 

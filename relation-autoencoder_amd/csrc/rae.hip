@@ -11,6 +11,7 @@
 //              deterministic gradient sums + AdaGrad/SGD in place (rae_update.hpp)
 //   k_dense_w + k_finalize_cost   only when lambda1/lambda2 != 0 (dense W regulariser)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdio>
@@ -298,7 +299,23 @@ struct rae_plan {
     int q = 1;
     unsigned long long* stamps_fwd = nullptr;
     unsigned long long* stamps_upd = nullptr;
+    hipEvent_t t_start = nullptr, t_stop = nullptr;   // armed by rae_time_next for ONE call
 };
+
+// Main-step launches go through here.  With a timing pair armed (rae_time_next) the kernels
+// are launched by hipExtLaunchKernelGGL: the start event takes the first kernel's dispatch
+// begin timestamp, the stop event the last kernel's end timestamp -- the kernels' execution
+// span as rocprofv3 --kernel-trace reports it, without the event packets' own overhead.
+#define RAE_LAUNCH(p, K, g, b, sh, st, ...)                                                 \
+    do {                                                                                  \
+        if ((p)->t_stop) {                                                                \
+            hipEvent_t e0_ = (p)->t_start;                                                \
+            (p)->t_start = nullptr;                                                       \
+            hipExtLaunchKernelGGL(K, g, b, sh, st, e0_, (p)->t_stop, 0, __VA_ARGS__);      \
+        } else {                                                                          \
+            hipLaunchKernelGGL(K, g, b, sh, st, __VA_ARGS__);                             \
+        }                                                                                 \
+    } while (0)
 
 extern "C" const char* rae_last_error(void) { return g_last_error.c_str(); }
 extern "C" int rae_version(void) { return RAE_VERSION; }
@@ -542,31 +559,31 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;
     const bool c2 = a.m == 30 && a.r == 100 && a.s == 10;
     if (c3 && p->v4)
-        hipLaunchKernelGGL((k_forward<true, DimsC3>), gr, bt, p->smem_fwd, st, a);
+        RAE_LAUNCH(p, (k_forward<true, DimsC3>), gr, bt, p->smem_fwd, st, a);
     else if (c2 && !p->v4)
-        hipLaunchKernelGGL((k_forward<false, DimsC2>), gr, bt, p->smem_fwd, st, a);
+        RAE_LAUNCH(p, (k_forward<false, DimsC2>), gr, bt, p->smem_fwd, st, a);
     else if (p->v4)
-        hipLaunchKernelGGL((k_forward<true, DynDims>), gr, bt, p->smem_fwd, st, a);
+        RAE_LAUNCH(p, (k_forward<true, DynDims>), gr, bt, p->smem_fwd, st, a);
     else
-        hipLaunchKernelGGL((k_forward<false, DynDims>), gr, bt, p->smem_fwd, st, a);
+        RAE_LAUNCH(p, (k_forward<false, DynDims>), gr, bt, p->smem_fwd, st, a);
 }
 
 template <bool V4>
 static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
-    hipLaunchKernelGGL((k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
+    RAE_LAUNCH(p, (k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
     const int gm = ceil_div(bil_m_tasks(a.l, a.r), RAE_NWAVE);
     if (V4 && a.bf16)
-        hipLaunchKernelGGL((k_bil_m<V4, true>), dim3(gm), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, (k_bil_m<V4, true>), dim3(gm), dim3(RAE_BT), 0, st, a);
     else
-        hipLaunchKernelGGL((k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
-    hipLaunchKernelGGL((k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
+        RAE_LAUNCH(p, (k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
+    RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
     if (a.bf16)
-        hipLaunchKernelGGL(k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
     else
-        hipLaunchKernelGGL(k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
-    hipLaunchKernelGGL(k_bil_fin, ge, dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
+    RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_BT), 0, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
@@ -578,6 +595,7 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     if (a.dec == RAE_DEC_SP) launch_fwd_sp(p, a, st);
     else if (p->v4) launch_fwd_bil<true>(p, a, st);
     else launch_fwd_bil<false>(p, a, st);
+    p->t_start = p->t_stop = nullptr;
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }
@@ -585,11 +603,11 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
 template <int OPT, bool V4, bool BIL>
 static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
     if constexpr (BIL) {
-        if (p->q == 1) hipLaunchKernelGGL((k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
-        else hipLaunchKernelGGL((k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
+        if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
+        else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
     } else {
-        if (p->q == 1) hipLaunchKernelGGL((k_update<OPT, V4, 1>), gu, bt, 0, st, a);
-        else hipLaunchKernelGGL((k_update<OPT, V4, 2>), gu, bt, 0, st, a);
+        if (p->q == 1) RAE_LAUNCH(p, (k_update<OPT, V4, 1>), gu, bt, 0, st, a);
+        else RAE_LAUNCH(p, (k_update<OPT, V4, 2>), gu, bt, 0, st, a);
     }
 }
 template <int OPT, bool V4>
@@ -614,13 +632,14 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     HIPCHK(hipGetLastError());
     if (a.reg_on) {
         if (a.opt == RAE_OPT_ADAGRAD)
-            hipLaunchKernelGGL((k_dense_w<0>), dim3(p->grid_dense), bt, 0, st, a);
+            RAE_LAUNCH(p, (k_dense_w<0>), dim3(p->grid_dense), bt, 0, st, a);
         else
-            hipLaunchKernelGGL((k_dense_w<1>), dim3(p->grid_dense), bt, 0, st, a);
+            RAE_LAUNCH(p, (k_dense_w<1>), dim3(p->grid_dense), bt, 0, st, a);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_finalize_cost, dim3(1), dim3(64), 0, st, a);
+        RAE_LAUNCH(p, k_finalize_cost, dim3(1), dim3(64), 0, st, a);
         HIPCHK(hipGetLastError());
     }
+    p->t_start = p->t_stop = nullptr;
     return RAE_OK;
 }
 
@@ -651,6 +670,31 @@ extern "C" int rae_step_forward(rae_plan* p, int64_t off, rae_stream_t stream) {
 extern "C" int rae_step_update(rae_plan* p, int64_t off, rae_stream_t stream) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     return launch_update(p, p->d_cursor, off, (hipStream_t)stream);
+}
+
+extern "C" int rae_time_next(rae_plan* p, void* start, void* stop) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (!start || !stop) return fail(RAE_E_INVALID, "null event");
+    p->t_start = (hipEvent_t)start;
+    p->t_stop = (hipEvent_t)stop;
+    return RAE_OK;
+}
+extern "C" int rae_event_create(void** ev) {
+    if (!ev) return fail(RAE_E_INVALID, "null argument");
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreate(&e));
+    *ev = (void*)e;
+    return RAE_OK;
+}
+extern "C" int rae_event_destroy(void* ev) {
+    if (ev) HIPCHK(hipEventDestroy((hipEvent_t)ev));
+    return RAE_OK;
+}
+extern "C" int rae_event_elapsed_ms(void* start, void* stop, float* ms) {
+    if (!start || !stop || !ms) return fail(RAE_E_INVALID, "null argument");
+    HIPCHK(hipEventSynchronize((hipEvent_t)stop));
+    HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return RAE_OK;
 }
 
 extern "C" int rae_train_step(rae_plan* p, int64_t batch, const int32_t* n1, const int32_t* n2,
