@@ -117,7 +117,10 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 template <int OPT, bool V4, int Q, bool BIL>
 __device__ __forceinline__ void update_body(const StepArgs& a) {
     const int lane = threadIdx.x & 63;
-    const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    // the wave index as a provably uniform value: every task index, row id and record
+    // offset derived from it is then scalar (s_load of the segment, SGPR soffsets, scalar
+    // branches) instead of VGPR-resident and exec-masked
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
     const int nw = gridDim.x * RAE_NWAVE;
     const int64_t g = *a.cursor + a.step_offset;
     const int64_t ex0 = g * (int64_t)a.L;
@@ -125,19 +128,37 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     const int nCt = n_ctiles(a.dec, a.r, a.m);
     const int nRt = n_rtiles(a.dec, a.r, a.m);
     const int64_t slot = g % a.index_window;
-    const int CA = a.hdrA[2 * slot], TA = a.hdrA[2 * slot + 1];
-    const int CW = a.hdrW[2 * slot], TW = a.hdrW[2 * slot + 1];
-    const int T = nCt + nRt + mt + 1 + TA + TW;
+    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];   // records, rows, heavy rows
+    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
+    const int TA = hA.y, HA = hA.z, TW = hW.y, HW = hW.z;
+    // Task order = dispatch order: the heavy rows (Zipf-frequent entities / features, the
+    // longest tasks) first, then the dense tiles and the cost, then the light rows.
+    const int nD = nCt + nRt + mt + 1;
+    const int T = TA + TW + nD;
 #ifdef RAE_STAMPS
     unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     int first_type = -1;
 #endif
     for (int t = gw; t < T; t += nw) {
-        int tt = t;
+        // task -> (kind, index): kind 0 C-tile, 1 R-tile, 2 Wb-tile, 3 cost, 4 A row, 5 W row;
+        // for rows, x = the segment slot (heavy x = u, light x = cap-1-v; rae_index.hpp)
+        int kind, x;
+        if (t < HA) { kind = 4; x = t; }
+        else if (t < HA + HW) { kind = 5; x = t - HA; }
+        else if (t < HA + HW + nD) {
+            x = t - HA - HW;
+            if (x < nCt) kind = 0;
+            else if ((x -= nCt) < nRt) kind = 1;
+            else if ((x -= nRt) < mt) kind = 2;
+            else { kind = 3; x = 0; }
+        } else {
+            const int v = t - HA - HW - nD;
+            if (v < TA - HA) { kind = 4; x = a.RA - 1 - v; }
+            else { kind = 5; x = a.RW - 1 - (v - (TA - HA)); }
+        }
 #ifdef RAE_STAMPS
         if (first_type < 0) {
-            first_type = t < nCt ? 0 : (t < nCt + nRt ? 1 : (t < nCt + nRt + mt ? 2 :
-                         (t < nCt + nRt + mt + 1 ? 3 : (t < nCt + nRt + mt + 1 + TA ? 4 : 5))));
+            first_type = (kind >= 4 && t < HA + HW) ? kind + 2 : kind;   // 6/7: heavy rows
             if (a.stamps && lane == 0) {
                 a.stamps[(size_t)gw * 4 + 0] = t_start;
                 a.stamps[(size_t)gw * 4 + 1] = (unsigned long long)first_type;
@@ -145,48 +166,28 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
         }
 #endif
 #ifdef RAE_SKIP_TILES
-        if (tt < nCt + nRt + mt + 1) continue;     // diagnostic: row tasks alone
+        if (kind < 4) continue;     // diagnostic: row tasks alone
 #endif
-        if (tt < nCt) {
-            const int which = tt / (rt * mt), ti = tt - which * rt * mt;
+#ifdef RAE_SKIP_ROWS
+        if (kind >= 4) continue;    // diagnostic: tile tasks alone
+#endif
+        if (kind == 0) {
+            const int which = x / (rt * mt), ti = x - which * rt * mt;
             task_mfma_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
                                 which ? a.lay.odw2 : a.lay.odw1, false, (ti / mt) * 16,
-                                (ti % mt) * 16, t, lane);
-            RAE_WAVE_END();
-            continue;
-        }
-        tt -= nCt;
-        if (BIL && tt < nRt) {
-            task_bilinear_rows<OPT>(a, tt, nCt + tt, lane);
-            RAE_WAVE_END();
-            continue;
-        }
-        tt -= nRt;
-        if (tt < mt) {
-            task_mfma_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, tt * 16, 0, lane);
-            RAE_WAVE_END();
-            continue;
-        }
-        tt -= mt;
-        if (tt == 0) {
+                                (ti % mt) * 16, x, lane);
+        } else if (BIL && kind == 1) {
+            task_bilinear_rows<OPT>(a, x, nCt + x, lane);
+        } else if (kind == 2) {
+            task_mfma_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, x * 16, 0, lane);
+        } else if (kind == 3) {
             task_cost(a, lane);
-            RAE_WAVE_END();
-            continue;
+        } else if (kind == 4) {
+            task_entity_row<OPT, V4, Q, BIL>(a, slot, x, lane);
+        } else {
+            task_feature_row<OPT, V4, Q>(a, ex0, slot, x, lane);
         }
-        tt -= 1;
-#ifdef RAE_SKIP_ROWS
-        if (true) continue;     // diagnostic: tile tasks alone
-#endif
-        if (tt < TA) {
-            task_entity_row<OPT, V4, Q, BIL>(a, slot, tt, TA, CA, lane);
-            RAE_WAVE_END();
-            continue;
-        }
-        tt -= TA;
-        task_feature_row<OPT, V4, Q>(a, ex0, slot, tt, TW, CW, lane);
-#ifdef RAE_STAMPS
-        if (a.stamps && lane == 0 && t == gw) a.stamps[(size_t)gw * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-#endif
+        RAE_WAVE_END();
     }
 }
 
@@ -451,9 +452,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     };
     const size_t o_cursor = take(8), o_zero = take(8), o_err = take(8), o_base = take(8);
     const size_t W_ = (size_t)a.index_window;
-    const size_t o_hdrA = take(8 * W_), o_hdrW = take(8 * W_);
-    const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(8ull * W_ * a.RA);
-    const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(8ull * W_ * a.RW);
+    const size_t o_hdrA = take(16 * W_), o_hdrW = take(16 * W_);
+    const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(16ull * W_ * a.RA);
+    const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(16ull * W_ * a.RW);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     const bool bil = c.decoder != RAE_DEC_SP;
@@ -488,7 +489,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    p->smem_idx = 8ull * RAE_KCAP + 4ull * (33 + L + 1);
+    p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP;
     p->smem_fwd = smem_ex;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
     if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024) {

@@ -9,6 +9,7 @@
 #define RAE_NWAVE (RAE_BT / RAE_WAVE)
 #define RAE_KCAP 8192         // LDS capacity (64-bit keys) of one row-index partition
 #define RAE_PART 256          // target records per row-index partition
+#define RAE_HEAVY 4           // a parameter row with more records than this per step is "heavy"
 
 namespace rae {
 
@@ -20,10 +21,12 @@ template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
     return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
 }
+// float form for the quad_perm / row mirror patterns only (every lane has a source in its
+// row): bound_ctrl lets the DPP-combine pass fold the move into its consumer
+// (v_add_f32_dpp / v_max_f32_dpp -- one instruction per reduction step instead of three)
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL,
-                                                      0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 // value of lane (lane ^ 16) / (lane ^ 32) via v_permlane16_swap / v_permlane32_swap
 __device__ __forceinline__ unsigned xor16_u32(unsigned v) {
@@ -188,6 +191,26 @@ __device__ __forceinline__ void vfma(float& acc, float s, float v) { acc += s * 
 __device__ __forceinline__ void vfma(float4& acc, float s, float4 v) {
     acc.x += s * v.x; acc.y += s * v.y; acc.z += s * v.z; acc.w += s * v.w;
 }
+// Exchange-record loads through one buffer resource: the record's offset rides in the scalar
+// soffset, the lane's column in a 32-bit voffset -- one SGPR per load instead of a 64-bit
+// address pair, which is what lets the update's wide rounds fit its 80-VGPR budget.
+// (dword3 0x00020000: the gfx9-family raw-buffer format word.)
+typedef unsigned rae_v4u __attribute__((ext_vector_type(4)));
+struct RecBuf {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ explicit RecBuf(const float* p)
+        : rs(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, -1, 0x00020000)) {}
+    // element offsets (floats): soff wave-uniform, voff per lane
+    __device__ __forceinline__ void load(float4& v, int voff, int soff) const {
+        const rae_v4u u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff * 4, soff * 4, 0);
+        v = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                        __uint_as_float(u.w));
+    }
+    __device__ __forceinline__ void load(float& v, int voff, int soff) const {
+        v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff * 4, soff * 4, 0));
+    }
+};
+
 __device__ __forceinline__ void vadd(float& acc, float v) { acc += v; }
 __device__ __forceinline__ void vadd(float4& acc, float4 v) {
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;

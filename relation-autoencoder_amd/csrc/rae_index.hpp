@@ -14,9 +14,14 @@
 // parameters -- so it is built ahead of the steps, for a window of batches per launch
 // (k_build_index, one workgroup per (batch, A|W)), off the step's critical path.
 // Layout per batch slot (slot = batch % window):
-//   hdr[slot]            = (records, unique rows)
+//   hdr[slot]            = (records, unique rows, heavy rows, 0)
 //   srec[slot][i]        = record id, i in sorted order
-//   seg[slot][u]         = (row, first sorted position) of unique row u
+//   seg[slot][x]         = (row, first sorted position, end position, first record id) of a
+//                          unique row; rows with more than RAE_HEAVY records ("heavy": the
+//                          Zipf-frequent entities / features) fill x = 0, 1, ... and the light
+//                          rows fill x = Rcap-1, Rcap-2, ... so the update can hand the heavy
+//                          rows -- its longest tasks -- to the first-dispatched waves, and a
+//                          one-record row needs no srec read (its record rides in the segment)
 // Records: A-index rec = b*NJ + j (j = 0 e1, 1 e2, 2+t neg1[t], 2+s+t neg2[t]);
 //          W-index rec = b << posbits | position of the feature in row b.
 // Rows are hash-partitioned (row % H) when a batch has more records than one LDS sort
@@ -76,15 +81,16 @@ template <int BT>
 __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bool isA,
                                   char* smem) {
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-    int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);   // [0] count, [1..16] scan scratch
+    int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);   // [0] count, [1..24] scan scratch
     int* sptr = sint + 32;                                   // batch indptr (W index)
+    int* sstart = sptr + a.L + 1;                            // segment starts of a partition
     const int tid = threadIdx.x;
     const int64_t ex0 = g * (int64_t)a.L;
     const int NJ = 2 + 2 * a.s;
     const int Rcap = isA ? a.RA : a.RW;
-    int32_t* hdr = (isA ? a.hdrA : a.hdrW) + 2 * slot;
+    int32_t* hdr = (isA ? a.hdrA : a.hdrW) + 4 * slot;
     int32_t* srec = (isA ? a.srecA : a.srecW) + slot * (int64_t)Rcap;
-    int32_t* seg = (isA ? a.urowA : a.urowW) + 2 * slot * (int64_t)Rcap;
+    int4* seg = reinterpret_cast<int4*>(isA ? a.urowA : a.urowW) + slot * (int64_t)Rcap;
     if (!isA)
         for (int b = tid; b <= a.L; b += BT) sptr[b] = a.indptr[ex0 + b];
     __syncthreads();
@@ -93,12 +99,12 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     if (nrec > Rcap) {
         if (tid == 0) {
             atomicOr(a.err, 4);
-            hdr[0] = hdr[1] = 0;
+            hdr[0] = hdr[1] = hdr[2] = 0;
         }
         return;
     }
     const int H = index_partitions(nrec);
-    int base_i = 0, base_u = 0;
+    int base_i = 0, nh = 0, nl = 0;
     for (int h = 0; h < H; ++h) {
         if (tid == 0) sint[0] = 0;
         __syncthreads();
@@ -133,7 +139,7 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
         if (cnt > RAE_KCAP) {
             if (tid == 0) {
                 atomicOr(a.err, isA ? 1 : 2);
-                hdr[0] = hdr[1] = 0;
+                hdr[0] = hdr[1] = hdr[2] = 0;
             }
             return;
         }
@@ -142,32 +148,53 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
         for (int i = cnt + tid; i < n2; i += BT) keys[i] = ~0ull;
         __syncthreads();
         lds_bitonic_sort<BT>(keys, n2);
+        // segment heads in sorted order -> sstart[local segment]
         int nu = 0;
         for (int i0 = 0; i0 < cnt; i0 += BT) {
             const int i = i0 + tid;
             int head = 0;
-            unsigned row = 0;
             if (i < cnt) {
                 const unsigned long long k = keys[i];
-                row = (unsigned)(k >> 32);
+                const unsigned row = (unsigned)(k >> 32);
                 head = (i == 0) || ((unsigned)(keys[i - 1] >> 32) != row);
                 srec[base_i + i] = (int32_t)(unsigned)(k & 0xffffffffull);
             }
             int tot;
-            const int u = base_u + nu + block_flag_scan<BT>(head, sint + 1, &tot);
-            if (head) {
-                seg[2 * u] = (int32_t)row;
-                seg[2 * u + 1] = base_i + i;
-            }
+            const int u = nu + block_flag_scan<BT>(head, sint + 1, &tot);
+            if (head) sstart[u] = i;
             nu += tot;
         }
+        __syncthreads();
+        // segments -> heavy rows at the front, light rows at the back (order kept in each)
+        for (int v0 = 0; v0 < nu; v0 += BT) {
+            const int v = v0 + tid;
+            const bool valid = v < nu;
+            int st = 0, en = 0;
+            if (valid) {
+                st = sstart[v];
+                en = (v + 1 < nu) ? sstart[v + 1] : cnt;
+            }
+            const bool heavy = valid && (en - st) > RAE_HEAVY;
+            int htot, ltot;
+            const int hp = block_flag_scan<BT>(heavy, sint + 1, &htot);
+            const int lp = block_flag_scan<BT>(valid && !heavy, sint + 12, &ltot);
+            if (valid) {
+                const unsigned long long k = keys[st];
+                const int x = heavy ? nh + hp : Rcap - 1 - (nl + lp);
+                seg[x] = make_int4((int)(unsigned)(k >> 32), base_i + st, base_i + en,
+                                   (int)(unsigned)(k & 0xffffffffull));
+            }
+            nh += htot;
+            nl += ltot;
+        }
         base_i += cnt;
-        base_u += nu;
         __syncthreads();
     }
     if (tid == 0) {
         hdr[0] = base_i;
-        hdr[1] = base_u;
+        hdr[1] = nh + nl;
+        hdr[2] = nh;
+        hdr[3] = 0;
     }
 }
 

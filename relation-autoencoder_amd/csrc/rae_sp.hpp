@@ -779,23 +779,28 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     const bool lv = lane < RV;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     const float4* Rv = reinterpret_cast<const float4*>(S.srows);
-    const float4 wc1 = lv ? reinterpret_cast<const float4*>(S.swC1)[lane] : z4;
-    const float4 wc2 = lv ? reinterpret_cast<const float4*>(S.swC2)[lane] : z4;
+    // branch-free: every lane reads a valid LDS float4 (lanes past the row re-read column 0)
+    // and is zeroed through wc, so all the wave's LDS reads issue back to back
+    const int lc = lv ? lane : 0;
+    float4 wc1 = reinterpret_cast<const float4*>(S.swC1)[lc];
+    float4 wc2 = reinterpret_cast<const float4*>(S.swC2)[lc];
+    if (!lv) wc1 = wc2 = z4;
     {
         constexpr int RPW = (NR + RAE_FNW - 1) / RAE_FNW;
         float d[RPW];
-        float d0b = 0.f;
+        float4 xr[RPW];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int rho = w + RAE_FNW * q;            // wave-uniform
+            xr[q] = Rv[(rho < NR ? rho : 0) * RV + lc];
+        }
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
             const int rho = w + RAE_FNW * q;
-            float v = 0.f;
-            if (rho < NR && lv) {
-                const float4 x = Rv[rho * RV + lane];
-                v = vdot(x, rho > s ? wc2 : wc1);          // rows 1..s: neg1, s+1..2s: neg2
-                if (rho == 0) d0b = vdot(x, wc2);
-            }
-            d[q] = v;
+            const float v = vdot(xr[q], rho > s ? wc2 : wc1);   // rows 1..s: neg1, s+1..2s: neg2
+            d[q] = rho < NR ? v : 0.f;
         }
+        float d0b = (w == 0) ? vdot(xr[0], wc2) : 0.f;
 #pragma unroll
         for (int q = 0; q < RPW; ++q) d[q] = wave_sum(d[q]);
         if (w == 0) d0b = wave_sum(d0b);

@@ -30,11 +30,15 @@ namespace rae {
 // SP/hybrid C1, C2: coef(b, i) = dw1_b[i] / dw2_b[i]; Wb (ones): one row of ones times dS_b.
 typedef float rae_f4 __attribute__((ext_vector_type(4)));
 #ifndef RAE_TU
-#define RAE_TU 8     // k-steps (x4 examples) whose operands are loaded before the MFMA chain
+#define RAE_TU 13    // k-steps (x4 examples) whose operands are loaded before the MFMA chain
+#endif
 #ifndef RAE_UNR1
-#define RAE_UNR1 4
+#define RAE_UNR1 4   // record vectors per round on light rows (Q = 1)
 #endif
+#ifndef RAE_UNRH
+#define RAE_UNRH 8   // record vectors per round on heavy rows (> RAE_UNR1 records; Q = 1)
 #endif
+template <int N> struct IntC { static constexpr int value = N; };
 
 template <int OPT>
 __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw,
@@ -68,16 +72,29 @@ __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows
         pw[reg] = M[o];
         pa[reg] = (OPT == 0) ? aM[o] : 0.f;
     }
+    // L % 4 == 0 (every k-step's 4 examples exist): the k-step's first record offset is
+    // wave-uniform and rides in the buffer load's soffset, the lane's (example, column) in
+    // one voffset VGPR for all TU loads
+    const RecBuf rb_(a.ex);
+    const bool whole = (L & 3) == 0;
+    const int rec = a.lay.rec, vx = lk * rec + ox, vy = lk * rec + oy;
     for (int b0 = 0; b0 < L; b0 += 4 * RAE_TU) {
         float av[RAE_TU], bv[RAE_TU];
         // every operand load goes out before the first MFMA: the sched_barrier keeps the
         // scheduler from sinking each load next to its MFMA (which serialised 32 round trips)
 #pragma unroll
         for (int u = 0; u < RAE_TU; ++u) {
-            const int b = b0 + 4 * u + lk;
-            const int rb = (b < L ? b : 0) * a.lay.rec;
-            av[u] = ones ? 1.f : a.ex[rb + ox];
-            bv[u] = a.ex[rb + oy];
+            const int bs = b0 + 4 * u;
+            if (whole) {
+                const int so = (bs < L ? bs : 0) * rec;
+                if (ones) av[u] = 1.f; else rb_.load(av[u], vx, so);
+                rb_.load(bv[u], vy, so);
+            } else {
+                const int b = bs + lk;
+                const int rb = (b < L ? b : 0) * rec;
+                av[u] = ones ? 1.f : a.ex[rb + ox];
+                bv[u] = a.ex[rb + oy];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -189,16 +206,15 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 // record) and broadcast with v_readlane (wave-uniform -> scalar addressing); the record
 // vectors are loaded UNR at a time with every load issued before the first FMA.
 template <int OPT, bool V4, int Q, bool XY>
-__device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, int C, int lane) {
+__device__ void task_entity_row(const StepArgs& a, int64_t slot, int x, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
+    constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
     typedef typename VecT<V4>::T VT;
     const int r = a.r, nv = r / VW, s = a.s, NJ = 2 + 2 * s;
     const int64_t base = slot * a.RA;
-    const int2 seg = reinterpret_cast<const int2*>(a.urowA + 2 * base)[u];
-    const int nxt = a.urowA[2 * base + 2 * (u + 1 < U ? u + 1 : u) + 1];
-    const int e = seg.x, st = seg.y;
-    const int en = (u + 1 < U) ? nxt : C;
+    const int4 seg = reinterpret_cast<const int4*>(a.urowA)[base + x];   // row, start, end, rec0
+    const int e = seg.x, st = seg.y, en = seg.z;
     float* prow = a.A + (int64_t)e * r;
     float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
     RowVec<V4, Q> pv, av, g;
@@ -209,9 +225,11 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, i
     g.zero();
     float gb = 0.f;
     const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;   // SP: e2 has no A gradient (c = 0)
+    const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
-        const int rec = a.srecA[base + c0 + (lane < n ? lane : 0)];
+        // a one-record row's record rides in its segment: no srec round trip
+        const int rec = (en - st == 1) ? seg.w : a.srecA[base + c0 + (lane < n ? lane : 0)];
         const int b = rec / NJ, j = rec - b * NJ;
         const int rb = b * a.lay.rec;
         const float* er = a.ex + rb + a.lay.ocoef + 2 * j;
@@ -220,26 +238,36 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, i
         if (lane >= n) cj = 0.f;
         gb += lane < n ? ga : 0.f;
         const int vo = rb + (j == 0 ? a.lay.oG1 : (j == 1 ? vo1 : (j < 2 + s ? a.lay.oV1 : a.lay.oV2)));
-        for (int k0 = 0; k0 < n; k0 += UNR) {
-            VT v[UNR][Q];
-            float ck[UNR];
+        // one round: U record vectors loaded (all issued before the first FMA), then summed
+        // in record order -- the same order for every U, so the round width is free
+        auto round = [&](auto Uc, int k0) {
+            constexpr int U = decltype(Uc)::value;
+            VT v[U][Q];
+            float ck[U];
 #pragma unroll
-            for (int k = 0; k < UNR; ++k) {
-                const int src = min(k0 + k, RAE_WAVE - 1);
+            for (int k = 0; k < U; ++k) {
+                const int src = min(k0 + k, n - 1);
                 const int ok = __builtin_amdgcn_readlane(vo, src);
                 ck[k] = (k0 + k < n) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj), src))
                                      : 0.f;
-                const VT* V = reinterpret_cast<const VT*>(a.ex + ok);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;
-                    v[k][q] = V[c < nv ? c : 0];
+                    rb_.load(v[k][q], (c < nv ? c : 0) * VW, ok);
                 }
             }
 #pragma unroll
-            for (int k = 0; k < UNR; ++k)
+            for (int k = 0; k < U; ++k)
 #pragma unroll
                 for (int q = 0; q < Q; ++q) vfma(g.v[q], ck[k], v[k][q]);
+        };
+        // Zipf-frequent entities carry tens of records per step: wide rounds keep their
+        // dependent round trips (the update's tail) few
+        if (n <= RAE_HEAVY && n <= UNR) {
+            round(IntC<UNR>{}, 0);
+        } else {
+#pragma clang loop unroll(disable)
+            for (int k0 = 0; k0 < n; k0 += UNRH) round(IntC<UNRH>{}, k0);
         }
     }
     gb = wave_sum(gb);
@@ -253,17 +281,15 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int u, int U, i
 
 // ---- W rows: g(W[f]) = sum over the row's CSR records of x_bf * dS_b ----------------------
 template <int OPT, bool V4, int Q>
-__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int u, int U,
-                                 int C, int lane) {
+__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int x, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
+    constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
     typedef typename VecT<V4>::T VT;
     const int m = a.m, nv = m / VW;
     const int64_t base = slot * a.RW;
-    const int2 seg = reinterpret_cast<const int2*>(a.urowW + 2 * base)[u];
-    const int nxt = a.urowW[2 * base + 2 * (u + 1 < U ? u + 1 : u) + 1];
-    const int f = seg.x, st = seg.y;
-    const int en = (u + 1 < U) ? nxt : C;
+    const int4 seg = reinterpret_cast<const int4*>(a.urowW)[base + x];   // row, start, end, rec0
+    const int f = seg.x, st = seg.y, en = seg.z;
     const unsigned mask = (1u << a.posbits) - 1u;
     float* prow = a.W + (int64_t)f * m;
     float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
@@ -273,33 +299,40 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
         if (OPT == 0) av.load(arow, nv, lane); else av.zero();
     }
     g.zero();
+    const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
-        const unsigned rec = (unsigned)a.srecW[base + c0 + (lane < n ? lane : 0)];
+        const unsigned rec = (unsigned)((en - st == 1) ? seg.w : a.srecW[base + c0 + (lane < n ? lane : 0)]);
         const int b = (int)(rec >> a.posbits);
         float val = 1.f;
         if (a.values) val = a.values[a.indptr[ex0 + b] + (int)(rec & mask)];
         if (lane >= n) val = 0.f;
-        for (int k0 = 0; k0 < n; k0 += UNR) {
-            VT v[UNR][Q];
-            float cv[UNR];
+        auto round = [&](auto Uc, int k0) {
+            constexpr int U = decltype(Uc)::value;
+            VT v[U][Q];
+            float cv[U];
 #pragma unroll
-            for (int k = 0; k < UNR; ++k) {
-                const int src = min(k0 + k, RAE_WAVE - 1);
+            for (int k = 0; k < U; ++k) {
+                const int src = min(k0 + k, n - 1);
                 const int bk = __builtin_amdgcn_readlane(b, src);
                 cv[k] = (k0 + k < n) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val), src))
                                      : 0.f;
-                const VT* dS = reinterpret_cast<const VT*>(a.ex + bk * a.lay.rec + a.lay.odS);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;
-                    v[k][q] = dS[c < nv ? c : 0];
+                    rb_.load(v[k][q], (c < nv ? c : 0) * VW, bk * a.lay.rec + a.lay.odS);
                 }
             }
 #pragma unroll
-            for (int k = 0; k < UNR; ++k)
+            for (int k = 0; k < U; ++k)
 #pragma unroll
                 for (int q = 0; q < Q; ++q) vfma(g.v[q], cv[k], v[k][q]);
+        };
+        if (n <= RAE_HEAVY && n <= UNR) {
+            round(IntC<UNR>{}, 0);
+        } else {                                    // Zipf-frequent features: wide rounds
+#pragma clang loop unroll(disable)
+            for (int k0 = 0; k0 < n; k0 += UNRH) round(IntC<UNRH>{}, k0);
         }
     }
     if (a.reg_on) {

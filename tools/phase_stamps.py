@@ -132,7 +132,7 @@ def main():
         ex = f[HA + HW:gf]
         clk += list((ex[:, 15] - ex[:, 14]) * 100.0 / ((ex[:, 7] - ex[:, 0]) * 100.0) * 100.0 / 100.0)
     print(f"  example-WG shader clock (s_memtime ticks / s_memrealtime): median {np.median(clk) * 100:.0f} MHz")
-    tnames = ["C-tile", "R-tile", "Wb-tile", "cost", "A-row", "W-row"]
+    tnames = ["C-tile", "R-tile", "Wb-tile", "cost", "A-row", "W-row", "A-heavy", "W-heavy"]
     allw = np.concatenate(up)
     valid = allw[:, 0] > 0
     allw = allw[valid]
