@@ -1,0 +1,78 @@
+"""Parity at BASELINE.json's full headline size (config 3: 1M synthetic triples, d = 2^17,
+K = 100, embed 200, neg 20, l = 100, SP decoder, AdaGrad) and at the config-4 shape.
+
+The HIP epoch path (graph-captured steps, device row index, sparse row updates) runs the
+first batches of an epoch; the float64 oracle runs the same batches with the reference's
+DENSE schedule (dense dW / dA, AdaGrad over every row, learning/Optimizers.py:27-33) from the
+same RandomState(2) initialisation and the same negatives.  At this size the row-index
+partitions, the heavy-row task ordering and the Zipf-frequent rows (tens of records per
+step) are all exercised, which the small golden cases cannot reach.
+
+Tolerances as in test_gpu_train.py: costs 2e-5 relative, parameters 2e-4 + 2e-3|p|; plus a
+size-independent property: every row the batches did not reference is bit-unchanged.
+"""
+import numpy as np
+import pytest
+
+import rae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+COST_RTOL = 2e-5
+
+
+def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234):
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    data, gold = synthetic_dataset(N, d, ntrue, seed=seed_data)
+    xs = data.split["train"]
+    tr = O.OracleTrainer("sp", xs.xFeats, xs.args1, xs.args2, data.negSamplingCum,
+                         np.random.RandomState(2), m, r, s, l, lr=0.1, alpha=1.0)
+    init = {k: v.copy() for k, v in tr.params.items()}
+    neg1 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+    neg2 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+    want = [tr.train_batch(b, neg1[:, O.batch_rows(b, l)], neg2[:, O.batch_rows(b, l)])
+            for b in range(steps)]
+
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "fullscale", "sp", False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2)
+    ind.compile_function()
+    eng = ind.engine
+    eng.set_epoch_negatives(neg1, neg2)
+    eng.run(0, steps)
+    torch.cuda.synchronize()
+    eng.check()
+    got = eng.costs[:steps].cpu().numpy().astype(np.float64)
+    params = {k: v.detach().cpu().double().numpy()
+              for k, v in ind.modelFunc.named_params().items()}
+    return np.array(want), got, tr.params, params, init
+
+
+def _check(want_c, got_c, want_p, got_p, init, min_untouched=0.0):
+    np.testing.assert_allclose(got_c, want_c, rtol=COST_RTOL, atol=0)
+    for k in want_p:
+        err = np.abs(got_p[k] - want_p[k])
+        tol = 2e-4 + 2e-3 * np.abs(want_p[k])
+        assert np.all(err <= tol), f"{k}: max err {err.max():.3e}"
+        # rows the batches never touched: bit-unchanged from the fp32 initialisation
+        if k in ("W", "A"):
+            untouched = np.all(want_p[k] == init[k], axis=1)
+            assert untouched.sum() >= min_untouched * untouched.size, k
+            f32 = init[k][untouched].astype(np.float32).astype(np.float64)
+            assert np.array_equal(got_p[k][untouched], f32), k
+
+
+def test_headline_c3_full_size(built_lib, cuda_dev):
+    want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=1_000_000, d=2 ** 17, m=100, r=200,
+                                              s=20, l=100, ntrue=100, steps=4)
+    _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
+
+
+def test_c4_shape(built_lib, cuda_dev):
+    # BASELINE config 4's K / embed / neg (K=300, embed 300, neg 50): the general (non-fixed
+    # shape) SP path, two float4 columns per lane in the row updates
+    want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=3000, d=20_000, m=300, r=300, s=50,
+                                              l=100, ntrue=20, steps=6)
+    _check(want_c, got_c, want_p, got_p, init)
