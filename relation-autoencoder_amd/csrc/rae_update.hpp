@@ -220,6 +220,12 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int x, int lane
     RowVec<V4, Q> pv, av, g;
     pv.load(prow, nv, lane);                     // parameters in flight with the records
     if (OPT == 0) av.load(arow, nv, lane); else av.zero();
+#ifdef RAE_STAMPS
+    if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
+        const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
+        a.stamps[(size_t)gw_ * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const float ab0 = a.Ab[e];
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
     g.zero();
@@ -298,6 +304,12 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
         pv.load(prow, nv, lane);
         if (OPT == 0) av.load(arow, nv, lane); else av.zero();
     }
+#ifdef RAE_STAMPS
+    if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
+        const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
+        a.stamps[(size_t)gw_ * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     g.zero();
     const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {

@@ -149,8 +149,13 @@ def main():
             d += list((sel[:, 2] - sel[:, 0]) / 100.0)
             st_ += list((sel[:, 0] - t0) / 100.0)
         if d:
+            extra = ""
+            if ty >= 4:
+                sg = np.concatenate([(v[v[:, 1] == ty][:, 3] - v[v[:, 1] == ty][:, 0]) / 100.0
+                                     for _, _, v in t0s])
+                extra = f"  (start->segment {np.median(sg):.2f}, segment->end {np.median(d) - np.median(sg):.2f})"
             print(f"    {nm:8s} n={len(d) // len(t0s):5d}  dur {np.median(d):.2f}/{np.max(d):.2f}"
-                  f"  start {np.median(st_):.2f}/{np.max(st_):.2f}")
+                  f"  start {np.median(st_):.2f}/{np.max(st_):.2f}{extra}")
     mids = []
     for t0, t1, v in t0s:
         sel = v[(v[:, 1] == 0) & (v[:, 3] > 0)]
