@@ -905,27 +905,63 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         float4 acc[CC_::CC];
 #pragma unroll
         for (int cc = 0; cc < CC_::CC; ++cc) acc[cc] = z4;
+        float d1[CC_::RA], d2[CC_::RA];              // branch-free: all LDS reads issue at once
 #pragma unroll
         for (int ra = 0; ra < CC_::RA; ++ra) {
             const int i = gid + RAE_NG * ra;
-            const float d1 = i < r ? S.sdw1[i] : 0.f;
-            const float d2 = i < r ? S.sdw2[i] : 0.f;
-#pragma unroll
-            for (int cc = 0; cc < CC_::CC; ++cc) {
-                vfma(acc[cc], d1, cc_.c1[ra][cc]);
-                vfma(acc[cc], d2, cc_.c2[ra][cc]);
-            }
+            d1[ra] = S.sdw1[i < r ? i : r - 1];
+            d2[ra] = S.sdw2[i < r ? i : r - 1];
         }
 #pragma unroll
-        for (int cc = 0; cc < CC_::CC; ++cc) {
-            float* v = reinterpret_cast<float*>(&acc[cc]);
+        for (int ra = 0; ra < CC_::RA; ++ra) {
+            const bool iv = gid + RAE_NG * ra < r;
+            const float e1 = iv ? d1[ra] : 0.f, e2 = iv ? d2[ra] : 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[e] += __uint_as_float(xor16_u32(__float_as_uint(v[e])));
-                v[e] += __uint_as_float(xor32_u32(__float_as_uint(v[e])));
+            for (int cc = 0; cc < CC_::CC; ++cc) {
+                vfma(acc[cc], e1, cc_.c1[ra][cc]);
+                vfma(acc[cc], e2, cc_.c2[ra][cc]);
             }
-            const int col = q + 16 * cc;
-            if (lane < 16 && col < MV) reinterpret_cast<float4*>(S.spart + w * mp)[col] = acc[cc];
+        }
+        if constexpr (CC_::CC == 2) {
+            // transpose-reduce the 8 partials over the wave's 4 lane groups with permlane
+            // swaps: each swap + add halves two values at once (6 swaps instead of 16), and
+            // leaves lane group G holding value {0,2,1,3}[G] of each float4
+            float* v0 = reinterpret_cast<float*>(&acc[0]);
+            float* v1 = reinterpret_cast<float*>(&acc[1]);
+            const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            float h[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {                 // xor-32 halves
+                const auto p = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(x[2 * k]), __float_as_uint(x[2 * k + 1]), false, false);
+                h[k] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+            }
+            float t[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {                 // xor-16 halves
+                const auto p = __builtin_amdgcn_permlane16_swap(
+                    __float_as_uint(h[2 * k]), __float_as_uint(h[2 * k + 1]), false, false);
+                t[k] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+            }
+            const int G = lane >> 4;
+            const int e = (G == 1) ? 2 : (G == 2 ? 1 : G);   // {0,2,1,3}[G]
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const int col = q + 16 * cc;
+                if (col < MV) S.spart[w * mp + 4 * col + e] = t[cc];
+            }
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < CC_::CC; ++cc) {
+                float* v = reinterpret_cast<float*>(&acc[cc]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] += __uint_as_float(xor16_u32(__float_as_uint(v[e])));
+                    v[e] += __uint_as_float(xor32_u32(__float_as_uint(v[e])));
+                }
+                const int col = q + 16 * cc;
+                if (lane < 16 && col < MV) reinterpret_cast<float4*>(S.spart + w * mp)[col] = acc[cc];
+            }
         }
     }
     lds_barrier();
