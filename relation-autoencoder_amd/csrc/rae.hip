@@ -94,7 +94,8 @@ typedef FixDims<30, 100, 10> DimsC2;
 __global__ __launch_bounds__(RAE_FBT) void k_build_index(StepArgs a, int64_t first) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = first + blockIdx.x;
-    build_batch_index<RAE_FBT>(a, g, g % a.index_window, blockIdx.y == 0, smem);
+    if (blockIdx.y == 2) build_batch_desc<RAE_FBT>(a, g, g % a.index_window);
+    else build_batch_index<RAE_FBT>(a, g, g % a.index_window, blockIdx.y == 0, smem);
 }
 
 __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
@@ -455,6 +456,14 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_hdrA = take(16 * W_), o_hdrW = take(16 * W_);
     const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(16ull * W_ * a.RA);
     const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(16ull * W_ * a.RW);
+    {
+        const int NJd = 2 + 2 * c.neg_samples;
+        int cap = c.max_row_nnz > 0 ? c.max_row_nnz : 1;
+        if (cap > 256) cap = 256;                    // the fast path's feature capacity
+        a.dcap = cap;
+        a.dstride = ((2 + NJd + cap) + 31) & ~31;     // whole 128-B lines per example
+    }
+    const size_t o_desc = take(4ull * W_ * c.batch_size * a.dstride);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     const bool bil = c.decoder != RAE_DEC_SP;
@@ -480,6 +489,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
 
+    a.desc = reinterpret_cast<int32_t*>(p->ws + o_desc);
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
     a.Mbuf = bil ? reinterpret_cast<float*>(p->ws + o_mbuf) : nullptr;
@@ -652,7 +662,7 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     if (count > p->args.index_window)
         return fail(RAE_E_INVALID, "more batches than the index window holds");
     if (count == 0) return RAE_OK;
-    hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 2), dim3(RAE_FBT), p->smem_idx, st,
+    hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 3), dim3(RAE_FBT), p->smem_idx, st,
                        p->args, first);
     HIPCHK(hipGetLastError());
     return RAE_OK;

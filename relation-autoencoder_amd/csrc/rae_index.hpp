@@ -198,4 +198,34 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     }
 }
 
+// Per-example descriptors of the rank's l examples of batch g (slot): everything the forward
+// needs before its W-row gather in ONE coalesced read -- the feature count and CSR start,
+// the NJ entity ids (e1, e2, neg1[t], neg2[t]) and the first dcap feature ids -- instead of
+// the dependent indptr -> indices -> W-row chain (parameter independent, so built ahead).
+template <int BT>
+__device__ void build_batch_desc(const StepArgs& a, int64_t g, int64_t slot) {
+    const int NJ = 2 + 2 * a.s, DS = a.dstride;
+    int32_t* out = a.desc + slot * (int64_t)a.l * DS;
+    for (int idx = threadIdx.x; idx < a.l * DS; idx += BT) {
+        const int bl = idx / DS, t = idx - bl * DS;
+        const int bg = a.rank * a.l + bl;
+        const int64_t ex = g * (int64_t)a.L + bg;
+        const int64_t col = a.neg_mode ? ex : (int64_t)bg;
+        const int p0 = a.indptr[ex];
+        int v = 0;
+        if (t == 0) v = a.indptr[ex + 1] - p0;
+        else if (t == 1) v = p0;
+        else if (t < 2 + NJ) {
+            const int j = t - 2;
+            v = (j == 0) ? a.args1[ex] : (j == 1) ? a.args2[ex]
+              : (j < 2 + a.s) ? a.neg1[(int64_t)(j - 2) * a.neg_stride + col]
+                              : a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
+        } else {
+            const int f = t - 2 - NJ;
+            if (f < a.dcap && f < a.indptr[ex + 1] - p0) v = a.indices[p0 + f];
+        }
+        out[idx] = v;
+    }
+}
+
 }  // namespace rae

@@ -648,7 +648,21 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 #endif
-    load_ids(a, Dm, ex, col, S);
+    // the example's descriptor (rae_index.hpp build_batch_desc): feature count, CSR start,
+    // entity ids and feature ids in one coalesced read
+    {
+        const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+        if (tid < a.dstride) {
+            const int v = dsc[tid];
+            if (tid == 0) S.sint[1] = v;                          // nf
+            else if (tid == 1) S.sint[0] = v;                     // p0
+            else if (tid < 2 + NJ) S.sids[tid - 2] = v;
+            else if (tid - 2 - NJ < 256) {
+                S.sfidx[tid - 2 - NJ] = v;
+                S.sfval[tid - 2 - NJ] = 1.f;
+            }
+        }
+    }
     constexpr int NI = mp / RAE_WAVE;
     float wbk[NI];                           // wave 0: the bias entries it reduces
 #pragma unroll
@@ -659,17 +673,16 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     if (tid == 0) S.sint[4] = 0;             // arrival counter of the W-row waves
     lds_barrier();
     RAE_STAMP(a, 1);
-    const int p0 = S.sint[0], nf = S.sint[1] - p0;
-    if (nf > 256) {                          // long feature rows: the general path
+    const int p0 = S.sint[0], nf = S.sint[1];
+    if (nf > a.dcap) {                       // longer than the descriptor holds: general path
         lds_barrier();
         sp_example<true, D>(a, g, bl, smem);
         return;
     }
-    if (w < 4 && tid < nf) {
-        S.sfidx[tid] = a.indices[p0 + tid];
-        S.sfval[tid] = a.values ? a.values[p0 + tid] : 1.f;
+    if (a.values) {                          // non-binary features: their values
+        if (w < 4 && tid < nf) S.sfval[tid] = a.values[p0 + tid];
+        lds_barrier();
     }
-    lds_barrier();
     RAE_STAMP(a, 10);
 
     // Per-CU issue order W rows -> A rows -> decoder matrices: vmcnt and the CU's memory
