@@ -183,7 +183,18 @@ def main():
     if K + W > nb:
         raise SystemExit(f"steps+warmup={K + W} exceed the {nb} global batches of one epoch")
 
-    eng.run(0, W)                          # includes graph capture
+    graphed = args.graph_chunk > 1
+    try:
+        eng.run(0, W)                      # includes graph capture
+    except RuntimeError as e:              # e.g. a collective the runtime cannot capture
+        if ws == 1 or not graphed:
+            raise
+        print(f"warning: graph capture of the data-parallel step failed ({e}); timing eager "
+              f"launches instead", file=sys.stderr)
+        graphed = False
+        eng.graph_chunk = 1
+        torch.cuda.synchronize()
+        eng.run(0, W)
     torch.cuda.synchronize()
     rdist.barrier()
     torch.cuda.synchronize()
@@ -321,7 +332,8 @@ def main():
                    "n_examples": cfg["N"], "n_features": cfg["d"], "relations": cfg["m"],
                    "embed": cfg["r"], "neg_samples": cfg["s"], "decoder": cfg["dec"],
                    "optimizer": "adagrad", "parallelism": f"dp{ws}",
-                   "n_entities": data.get_arg_voc_size(), "graph_chunk": args.graph_chunk},
+                   "n_entities": data.get_arg_voc_size(),
+                   "graph_chunk": args.graph_chunk if graphed else 1},
         "roofline": roof,
         "kernels": kern,
         "kernel_us": {"forward": fwd_us, "update": upd_us,
