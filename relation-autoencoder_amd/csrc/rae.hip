@@ -108,7 +108,7 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 #ifdef RAE_STAMPS
 #define RAE_WAVE_END()                                                                      \
     do {                                                                                    \
-        if (a.stamps && lane == 0 && t == gw)                                               \
+        if (a.stamps && lane == 0)      /* end of the wave's LAST task */                    \
             a.stamps[(size_t)gw * 4 + 2] = __builtin_amdgcn_s_memrealtime();                 \
     } while (0)
 #else

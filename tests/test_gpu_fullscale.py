@@ -76,3 +76,12 @@ def test_c4_shape(built_lib, cuda_dev):
     want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=3000, d=20_000, m=300, r=300, s=50,
                                               l=100, ntrue=20, steps=6)
     _check(want_c, got_c, want_p, got_p, init)
+
+
+def test_c3_global_batch_800(built_lib, cuda_dev):
+    # the global batch of 8 data-parallel ranks at l = 100: Zipf-frequent rows carry hundreds
+    # of records per step (workgroup rows split over four waves) and every K-chunk of the
+    # dense tiles is non-trivial
+    want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=1_000_000, d=2 ** 17, m=100, r=200,
+                                              s=20, l=800, ntrue=100, steps=3)
+    _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)

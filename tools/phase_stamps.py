@@ -154,7 +154,7 @@ def main():
                 sg = np.concatenate([(v[v[:, 1] == ty][:, 3] - v[v[:, 1] == ty][:, 0]) / 100.0
                                      for _, _, v in t0s])
                 extra = f"  (start->segment {np.median(sg):.2f}, segment->end {np.median(d) - np.median(sg):.2f})"
-            print(f"    {nm:8s} n={len(d) // len(t0s):5d}  dur {np.median(d):.2f}/{np.max(d):.2f}"
+            print(f"    {nm:8s} n={len(d) // len(t0s):5d}  busy {np.median(d):.2f}/{np.max(d):.2f}"
                   f"  start {np.median(st_):.2f}/{np.max(st_):.2f}{extra}")
     mids = []
     for t0, t1, v in t0s:
@@ -163,6 +163,12 @@ def main():
     if mids:
         mids = np.array(mids)
         print(f"  icache test C-tile: start->rep1 {np.median(mids[:, 0]):.2f}  rep1->end {np.median(mids[:, 1]):.2f}")
+    ends = np.concatenate([(v[:, 2] - t0) / 100.0 for t0, t1, v in t0s])
+    starts = np.concatenate([(v[:, 0] - t0) / 100.0 for t0, t1, v in t0s])
+    q = [10, 50, 90, 99, 100]
+    print("  update waves (" + str(len(ends) // len(t0s)) + "): first-start pct " +
+          " ".join(f"p{p} {np.percentile(starts, p):.2f}" for p in q) +
+          " | last-end pct " + " ".join(f"p{p} {np.percentile(ends, p):.2f}" for p in q))
     print(f"  update span: median {np.median([(t1 - t0) / 100.0 for t0, t1, _ in t0s]):.2f} us")
 
 
