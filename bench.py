@@ -314,6 +314,27 @@ def main():
                  "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label)"}
         del lab, pr
 
+    # ---- measured copy bandwidth of this HBM (STREAM-style float4 copy by torch, 1 GiB each
+    # way): the practical ceiling next to the 8 TB/s spec the roofline fractions quote
+    hbm_copy = None
+    if not args.no_label_pass:
+        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        ce = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(5)]
+        for a_, b_ in ce:
+            a_.record(st)
+            dst.copy_(src)
+            b_.record(st)
+        torch.cuda.synchronize()
+        cus = float(np.median([a_.elapsed_time(b_) for a_, b_ in ce]) * 1e3)
+        hbm_copy = {"GBs": 2 * src.numel() * 4 / (cus * 1e-6) / 1e9, "bytes": 2 * src.numel() * 4,
+                    "us": cus, "how": "torch device copy of a 1 GiB fp32 buffer (read + write), median of 5"}
+        if label is not None:
+            label["frac_of_measured_copy"] = label["achieved"] / hbm_copy["GBs"]
+        del src, dst
+
     ms_per_step = 1e3 * elapsed / K
     out = {
         "metric": METRIC,
@@ -341,6 +362,7 @@ def main():
                       "forward_p50": float(np.median(fwd_ms) * 1e3),
                       "update_p50": float(np.median(upd_ms) * 1e3)},
         "label_pass": label,
+        "hbm_copy": hbm_copy,
         "negative_sampling_s": t_neg,
         "negative_sampling": "host RandomState uniforms (reference stream) + device CDF search",
         "dataset_build_s": t_data,

@@ -146,6 +146,13 @@ int rae_step_forward(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
 /* K2 (+K3 when lambda1/lambda2 != 0): deterministic per-row gradient reduction over the
  * global batch and the optimizer update of every parameter; writes costs[batch].        */
 int rae_step_update(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
+/* The same two phases for an absolute global batch index (no device cursor: the index is a
+ * launch argument; rae_train_step runs this way).  Measured on MI355X: no faster than the
+ * cursor form inside graphs (the cursor load overlaps the kernels' other start-up loads),
+ * and per-chunk graphs cost more to replay than one graph replayed over an epoch window.
+ * `batch` in [0, n_examples / (batch_size * world_size)).                                */
+int rae_step_forward_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
+int rae_step_update_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
 /* One whole func['train'](batch_index, neg1, neg2) call on a single rank:
  * rae_set_negatives(PER_CALL) + index + forward + update for `batch_index`.            */
 int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,

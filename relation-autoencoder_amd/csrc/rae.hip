@@ -14,6 +14,7 @@
 #include <hip/hip_ext.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -42,7 +43,7 @@ template <bool V4, class D>
 __global__ __launch_bounds__(RAE_FBT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int64_t g = *a.cursor + a.step_offset;
+    const int64_t g = step_batch(a);
     if constexpr (D::fixed && V4) sp_example_fast<D>(a, g, blockIdx.x, smem);
     else sp_example<V4, D>(a, g, blockIdx.x, smem);
 }
@@ -51,7 +52,7 @@ void k_forward(StepArgs a) {
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bil_encode<V4>(a, *a.cursor + a.step_offset, blockIdx.x, smem);
+    bil_encode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
 __host__ __device__ inline int bil_m_tasks(int l, int r) {
     return ((l + 15) / 16) * (int)(((int64_t)r * r + 63) / 64);
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_m(StepArgs a) {
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_bil_dec(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bil_decode<V4>(a, *a.cursor + a.step_offset, blockIdx.x, smem);
+    bil_decode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
 __host__ __device__ inline int bil_dp_tasks(int l, int m, int nib) {
     return ((l + 15) / 16) * ((m + 15) / 16) * nib;
@@ -77,6 +78,11 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_dp(StepArgs a) {
     if (t >= bil_dp_tasks(a.l, a.m, a.nib)) return;
     if constexpr (BF16) bil_gemm_dp_bf16(a, t, threadIdx.x & 63);
     else bil_gemm_dp(a, t, threadIdx.x & 63);
+}
+template <int NJS, int MT>
+__global__ __launch_bounds__(RAE_BT) void k_bil_dp2(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bil_gemm_dp2<NJS, MT>(a, blockIdx.x, smem);
 }
 __global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
     __shared__ float sdp[1024];
@@ -123,7 +129,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     // branches) instead of VGPR-resident and exec-masked
     const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
     const int nw = gridDim.x * RAE_NWAVE;
-    const int64_t g = *a.cursor + a.step_offset;
+    const int64_t g = step_batch(a);
     const int64_t ex0 = g * (int64_t)a.L;
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
     const int nCt = n_ctiles(a.dec, a.r, a.m);
@@ -258,7 +264,7 @@ __global__ void k_finalize_cost(StepArgs a) {
         L1 += a.regpart[2 * (a.nregC + i)];
         L2 += a.regpart[2 * (a.nregC + i) + 1];
     }
-    const int64_t batch = *a.cursor + a.step_offset;
+    const int64_t batch = step_batch(a);
     a.costs[batch] = (float)((double)*a.base_cost + (double)a.l1adj * L1 + (double)a.l2adj * L2);
 }
 
@@ -299,6 +305,7 @@ struct rae_plan {
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
     int q = 1;
+    int dp2 = 0;            // bf16 dP kernel: 0 none (bil_gemm_dp*), 1 k_bil_dp2<7,7>, 2 <8,8>
     unsigned long long* stamps_fwd = nullptr;
     unsigned long long* stamps_upd = nullptr;
     hipEvent_t t_start = nullptr, t_stop = nullptr;   // armed by rae_time_next for ONE call
@@ -467,8 +474,16 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     const bool bil = c.decoder != RAE_DEC_SP;
-    a.nib = bil ? (c.embed + RAE_IB - 1) / RAE_IB : 0;
     a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
+    // bf16 dP with LDS-staged R slices (k_bil_dp2): the C5 shape compiled exactly, other
+    // shapes up to r = 256, K = 128 padded; float4 rows needed (r, K multiples of 4)
+    p->dp2 = 0;
+    const char* dp2env = getenv("RAE_DP2");      // diagnostic override: 0 = strided kernel
+    if (a.bf16 && c.embed % 4 == 0 && c.relations % 4 == 0 && !(dp2env && dp2env[0] == '0')) {
+        if ((c.embed + 31) / 32 == 7 && (c.relations + 15) / 16 == 7) p->dp2 = 1;
+        else if (c.embed <= 256 && c.relations <= 128) p->dp2 = 2;
+    }
+    a.nib = bil ? (p->dp2 ? (c.embed + RAE_IB2 - 1) / RAE_IB2 : (c.embed + RAE_IB - 1) / RAE_IB) : 0;
     const size_t o_mbuf = bil ? take(4ull * c.batch_size * c.embed * c.embed) : 0;
     const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
@@ -521,6 +536,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p->smem_fwd);
         if (bil) {
+            (void)hipFuncSetAttribute((const void*)k_bil_dp2<7, 7>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<7, 7>());
+            (void)hipFuncSetAttribute((const void*)k_bil_dp2<8, 8>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<8, 8>());
             (void)hipFuncSetAttribute((const void*)k_bil_dec<true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
             (void)hipFuncSetAttribute((const void*)k_bil_dec<false>,
@@ -590,7 +609,12 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
         RAE_LAUNCH(p, (k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
     RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
-    if (a.bf16)
+    const size_t lds77 = dp2_lds_bytes<7, 7>(), lds88 = dp2_lds_bytes<8, 8>();
+    if (p->dp2 == 1)
+        RAE_LAUNCH(p, (k_bil_dp2<7, 7>), dim3(a.nib), dim3(RAE_BT), lds77, st, a);
+    else if (p->dp2 == 2)
+        RAE_LAUNCH(p, (k_bil_dp2<8, 8>), dim3(a.nib), dim3(RAE_BT), lds88, st, a);
+    else if (a.bf16)
         RAE_LAUNCH(p, k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
     else
         RAE_LAUNCH(p, k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
@@ -683,6 +707,23 @@ extern "C" int rae_step_update(rae_plan* p, int64_t off, rae_stream_t stream) {
     return launch_update(p, p->d_cursor, off, (hipStream_t)stream);
 }
 
+// absolute-batch forms: the batch index rides in the launch (no device cursor)
+static int check_batch(rae_plan* p, int64_t batch) {
+    const int64_t nb = p->cfg.n_examples / ((int64_t)p->cfg.batch_size * p->cfg.world_size);
+    if (batch < 0 || batch >= nb) return fail(RAE_E_INVALID, "batch index out of the epoch");
+    return RAE_OK;
+}
+extern "C" int rae_step_forward_at(rae_plan* p, int64_t batch, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (int rc = check_batch(p, batch)) return rc;
+    return launch_forward(p, nullptr, batch, (hipStream_t)stream);
+}
+extern "C" int rae_step_update_at(rae_plan* p, int64_t batch, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (int rc = check_batch(p, batch)) return rc;
+    return launch_update(p, nullptr, batch, (hipStream_t)stream);
+}
+
 extern "C" int rae_time_next(rae_plan* p, void* start, void* stop) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     if (!start || !stop) return fail(RAE_E_INVALID, "null event");
@@ -719,9 +760,9 @@ extern "C" int rae_train_step(rae_plan* p, int64_t batch, const int32_t* n1, con
     if (rc) return rc;
     rc = launch_index(p, batch, 1, (hipStream_t)stream);
     if (rc) return rc;
-    rc = launch_forward(p, p->d_zero, batch, (hipStream_t)stream);
+    rc = launch_forward(p, nullptr, batch, (hipStream_t)stream);
     if (rc) return rc;
-    return launch_update(p, p->d_zero, batch, (hipStream_t)stream);
+    return launch_update(p, nullptr, batch, (hipStream_t)stream);
 }
 
 #ifdef RAE_STAMPS

@@ -252,6 +252,155 @@ __device__ void bil_gemm_dp_bf16(const StepArgs& a, int t, int lane) {
     }
 }
 
+// ---- k_bil_dp2: the bf16 dP contraction with the R slices staged in LDS -----------------------
+// dP_b[k] = sum_i sum_j U_b[i,j] R[i][j][k],  U_b[i,j] = x_b[i] a2_b[j] + a1_b[i] y_b[j].
+// One workgroup per block of RAE_IB2 rows i: the block's R[i] slices (r x m fp32, j-major)
+// are staged ONCE into LDS as bf16 in (k, j) order -- the B fragment of
+// v_mfma_f32_16x16x32_bf16 (8 consecutive j at one k) is then one ds_read_b128 -- and
+// every (16 examples x 16 relations) tile of the rank's batch reads them from there, so R
+// leaves HBM once per step instead of once per example tile through 4-byte strided loads
+// (bil_gemm_dp_bf16).  A wave owns whole example tiles: it holds the tile's a2 / y for all
+// j in registers (NJS x 8 per lane each) and runs all MT relation tiles, so U is built once
+// per (i, 32-wide j step) and reused MT times.  Partial sums per i-block -> dPpart, summed
+// in block order by bil_finish (deterministic).  Shapes: r <= 32 NJS, m <= 16 MT,
+// r % 4 == m % 4 == 0.
+#define RAE_IB2 2    // i rows per k_bil_dp2 workgroup (the q-loop selects x/a1 for q < 2)
+template <int NJS, int MT>
+constexpr size_t dp2_lds_bytes() { return (size_t)RAE_IB2 * MT * 16 * (NJS * 32 + 8) * 2; }
+template <int NJS, int MT>
+__device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
+    // LDS row stride JS = JP + 8 bf16: 16-B aligned fragment reads, and the 16 rows k a
+    // fragment read touches land on distinct bank groups
+    constexpr int JP = NJS * 32, KP = MT * 16, JS = JP + 8;
+    const int l = a.l, m = a.m, r = a.r;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, g = lane >> 4;
+    __bf16* lds = reinterpret_cast<__bf16*>(smem);
+    const int i0 = ib * RAE_IB2;
+    const int ni = min(RAE_IB2, r - i0);
+    // stage: R[i0+q][j][k] -> lds[q][k][j] (bf16, round to nearest even); the padding
+    // (j >= r, k >= m) is zero.
+    for (int e = tid; e < RAE_IB2 * KP * JS / 8; e += RAE_BT)
+        reinterpret_cast<uint4*>(lds)[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    // A staging unit is 8 rows j x one float4 of k: its 8 loads are lanes' consecutive
+    // 16-B chunks of whole rows (coalesced), and its 4 LDS stores are 16-B runs of 8 j at
+    // one k (ds_write_b128).  All of a slice's loads are issued before its first store.
+    const int m4 = m / 4, r8 = (r + 7) / 8, nunit = r8 * m4;
+    constexpr int UU = ((JP / 8) * (KP / 4) + RAE_BT - 1) / RAE_BT;
+    for (int q = 0; q < ni; ++q) {
+        const float4* src = reinterpret_cast<const float4*>(a.R3 + (int64_t)(i0 + q) * r * m);
+        __bf16* dst = lds + q * KP * JS;
+        float4 v[UU][8];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            const int e = tid + u * RAE_BT;
+            const bool ok = e < nunit;
+            const int jb = ok ? e / m4 : 0, kq = ok ? e - jb * m4 : 0;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                const int j = 8 * jb + h;
+                v[u][h] = src[(j < r ? j : 0) * m4 + kq];
+                if (j >= r) v[u][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            const int e = tid + u * RAE_BT;
+            if (e < nunit) {
+                const int jb = e / m4, kq = e - jb * m4;
+                __bf16* d = dst + 4 * kq * JS + 8 * jb;
+                rae_bf16x8 c0, c1, c2, c3;
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    c0[h] = (__bf16)v[u][h].x;
+                    c1[h] = (__bf16)v[u][h].y;
+                    c2[h] = (__bf16)v[u][h].z;
+                    c3[h] = (__bf16)v[u][h].w;
+                }
+                *reinterpret_cast<rae_bf16x8*>(d) = c0;
+                *reinterpret_cast<rae_bf16x8*>(d + JS) = c1;
+                *reinterpret_cast<rae_bf16x8*>(d + 2 * JS) = c2;
+                *reinterpret_cast<rae_bf16x8*>(d + 3 * JS) = c3;
+            }
+        }
+    }
+    __syncthreads();
+    const int nbt = (l + 15) / 16;
+    for (int bt = w; bt < nbt; bt += RAE_NWAVE) {
+        const int b = bt * 16 + li;
+        const bool bv = b < l;
+        const float* er = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec;
+        // a2 / y of the lane's example, all j (unconditional loads of clamped addresses,
+        // then selects: no exec-masked branches)
+        float4 a2v[NJS][2], yv[NJS][2];
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int js = 0; js < NJS; ++js) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = js * 32 + 8 * g + 4 * h;
+                const bool ok = bv && j < r;
+                const int jc = ok ? j : 0;
+                const float4 va = *reinterpret_cast<const float4*>(er + a.lay.oA2 + jc);
+                const float4 vy = *reinterpret_cast<const float4*>(er + a.lay.oY + jc);
+                a2v[js][h] = ok ? va : z;
+                yv[js][h] = ok ? vy : z;
+            }
+        }
+        float xq[RAE_IB2], aq[RAE_IB2];
+#pragma unroll
+        for (int q = 0; q < RAE_IB2; ++q) {
+            const bool ok = bv && q < ni;
+            const int ic = i0 + (q < ni ? q : 0);
+            const float xv = er[a.lay.oX + ic], av = er[a.lay.oA1 + ic];
+            xq[q] = ok ? xv : 0.f;
+            aq[q] = ok ? av : 0.f;
+        }
+        rae_bf4 acc[MT];
+#pragma unroll
+        for (int kt = 0; kt < MT; ++kt) acc[kt] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+        // software pipeline within each i: the next j step's MT B fragments are read from
+        // LDS while the current step's MFMAs run
+        rae_bf16x8 rb[2][MT];
+#pragma unroll 1
+        for (int q = 0; q < RAE_IB2; ++q) {
+            const __bf16* lq = lds + q * KP * JS + 8 * g + li * JS;
+#pragma unroll
+            for (int kt = 0; kt < MT; ++kt)
+                rb[0][kt] = *reinterpret_cast<const rae_bf16x8*>(lq + kt * 16 * JS);
+            const float xv = xq[0] * (q == 0) + xq[RAE_IB2 - 1] * (q != 0);
+            const float av = aq[0] * (q == 0) + aq[RAE_IB2 - 1] * (q != 0);
+#pragma unroll
+            for (int js = 0; js < NJS; ++js) {
+                if (js + 1 < NJS) {
+#pragma unroll
+                    for (int kt = 0; kt < MT; ++kt)
+                        rb[(js + 1) & 1][kt] =
+                            *reinterpret_cast<const rae_bf16x8*>(lq + kt * 16 * JS + (js + 1) * 32);
+                }
+                const float* p2 = reinterpret_cast<const float*>(&a2v[js][0]);
+                const float* py = reinterpret_cast<const float*>(&yv[js][0]);
+                rae_bf16x8 ua;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ua[e] = (__bf16)(xv * p2[e] + av * py[e]);
+#pragma unroll
+                for (int kt = 0; kt < MT; ++kt)
+                    acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, rb[js & 1][kt], acc[kt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int kt = 0; kt < MT; ++kt) {
+            const int k = kt * 16 + li;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int bo = bt * 16 + g * 4 + reg;
+                if (bo < l && k < m) a.dPpart[((int64_t)ib * l + bo) * m + k] = acc[kt][reg];
+            }
+        }
+    }
+}
+
 // ---- k_bil_dec helpers ----------------------------------------------------------------------
 struct BilSmem {
     float *v, *w, *a1, *a2, *wC1, *wC2, *x, *y, *My, *Mtx, *dw1, *dw2, *rows, *part, *dots, *Abv,
@@ -560,6 +709,7 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
     float sd = 0.f, sz = 0.f;
     for (int k = threadIdx.x; k < m; k += RAE_BT) {
         float dp = 0.f;
+#pragma unroll 10
         for (int ib = 0; ib < a.nib; ++ib) dp += a.dPpart[((int64_t)ib * l + bl) * m + k];
         if (hybrid) {
             float h = 0.f;

@@ -101,6 +101,13 @@ struct StepArgs {
     unsigned long long* stamps;   // diagnostic build only (RAE_STAMPS): phase timestamps
 };
 
+// The global batch a step kernel works on: a device cursor + offset (graphs replayed over an
+// epoch window), or -- cursor == nullptr -- the absolute batch baked into the launch (graphs
+// captured per chunk of the epoch; no dependent cursor load at kernel start).
+__device__ __forceinline__ int64_t step_batch(const StepArgs& a) {
+    return a.cursor ? *a.cursor + a.step_offset : a.step_offset;
+}
+
 #ifdef RAE_STAMPS
 #define RAE_STAMP(a, slot)                                                                  \
     do {                                                                                    \

@@ -144,7 +144,7 @@ __device__ void task_cost(const StepArgs& a, int lane) {
     if (lane == 0) {
         const double D = 4.0 * a.L + 2.0 * a.L * a.s;
         const float cost = (float)(-loss / D);
-        const int64_t batch = *a.cursor + a.step_offset;
+        const int64_t batch = step_batch(a);
         if (a.reg_on) *a.base_cost = cost;
         else a.costs[batch] = cost;
     }

@@ -23,6 +23,7 @@ EXPORTS = (
     "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version",
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
     "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
+    "rae_step_forward_at", "rae_step_update_at",
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
@@ -85,6 +86,8 @@ def load(path: str | None = None):
     lib.rae_advance_cursor.argtypes = [_P, C.c_int64, _P]
     lib.rae_step_forward.argtypes = [_P, C.c_int64, _P]
     lib.rae_step_update.argtypes = [_P, C.c_int64, _P]
+    lib.rae_step_forward_at.argtypes = [_P, C.c_int64, _P]
+    lib.rae_step_update_at.argtypes = [_P, C.c_int64, _P]
     lib.rae_train_step.argtypes = [_P, C.c_int64, _P, _P, _P]
     lib.rae_check.argtypes = [_P]
     lib.rae_build_index.argtypes = [_P, C.c_int64, C.c_int64, _P]
@@ -100,6 +103,7 @@ def load(path: str | None = None):
     for fn in ("rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
                "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
+               "rae_step_forward_at", "rae_step_update_at",
                "rae_check", "rae_label", "rae_build_index"):
         getattr(lib, fn).restype = C.c_int
     if path is None:

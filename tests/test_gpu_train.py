@@ -260,3 +260,68 @@ def test_bf16_mfma_path_tracks_oracle(built_lib, cuda_dev, dec):
     for k, v in tr.params.items():
         rel = np.linalg.norm(got[k] - v) / max(np.linalg.norm(v), 1e-12)
         assert rel < 2e-2, f"{k}: relative distance {rel:.3e}"
+
+
+def test_cursor_and_absolute_batch_launches_agree(built_lib, cuda_dev):
+    # the two ways include/rae.h addresses a step's batch: a device cursor + offset
+    # (rae_step_forward / rae_step_update) and the absolute index in the launch
+    # (rae_step_*_at; the func['train'] path rae_train_step uses it) -- bit-identical training
+    import ctypes as C
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    out = []
+    for mode in ("cursor", "absolute"):
+        data, gold = synthetic_dataset(600, 900, 5, seed=11)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 40, 24, 12, 5,
+                                 0.0, 0.0, "adagrad", "abs", "sp", False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=3)
+        ind.compile_function()
+        eng = ind.engine
+        n1, n2 = ind.draw_epoch_negatives()
+        eng.set_epoch_negatives(n1, n2)
+        nb = eng.nb
+        lib, st = eng.lib, C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert lib.rae_build_index(eng.plan, 0, nb, st) == 0
+        if mode == "absolute":
+            for b in range(nb):
+                assert lib.rae_step_forward_at(eng.plan, b, st) == 0
+                assert lib.rae_step_update_at(eng.plan, b, st) == 0
+        else:
+            assert lib.rae_set_cursor(eng.plan, 0, st) == 0
+            for i in range(nb):
+                assert lib.rae_step_forward(eng.plan, i, st) == 0
+                assert lib.rae_step_update(eng.plan, i, st) == 0
+        torch.cuda.synchronize()
+        eng.check()
+        out.append((_params(ind), eng.costs[:nb].cpu().numpy().copy()))
+    for k in out[0][0]:
+        assert np.array_equal(out[0][0][k], out[1][0][k]), k
+    assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("shape", [(100, 200, 20, 100), (60, 96, 5, 40)], ids=["c5", "padded"])
+@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
+def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
+    """The LDS-staged bf16 dP kernel (k_bil_dp2, compiled for the C5 shape and padded for
+    others) against the strided bf16 kernel it replaces (RAE_DP2=0): the same bf16 operands,
+    only the fp32 summation order differs, so whole runs agree to 1e-4 relative Frobenius
+    distance -- far inside the bf16-vs-float64 tolerance above (which both kernels meet
+    equally: tools/bf16_check.py)."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = shape
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RAE_DP2", flag)
+        data, gold = synthetic_dataset(200, 2000, 10, seed=99)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0,
+                                 0.0, "adagrad", "dp2", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True)
+        ind.learn(verbose=False)
+        out.append((_params(ind), np.array(ind.epoch_costs)))
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-5)
+    for k in out[0][0]:
+        a, b = out[0][0][k], out[1][0][k]
+        rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
+        assert rel < 1e-4, f"{k}: relative distance {rel:.3e}"

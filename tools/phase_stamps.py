@@ -71,15 +71,14 @@ def main():
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     fw, up = [], []
     lib.rae_build_index(eng.plan, 20, args.iters, st)
-    lib.rae_set_cursor(eng.plan, 20, st)
     for it in range(args.iters):
         bf = torch.zeros(gf * 16, dtype=torch.int64, device=dev)
         bu = torch.zeros(gu * 4 * 4, dtype=torch.int64, device=dev)
         lib.rae_debug_stamps(eng.plan, C.c_void_p(bf.data_ptr()), 1)
-        lib.rae_step_forward(eng.plan, it, st)
+        lib.rae_step_forward_at(eng.plan, 20 + it, st)
         torch.cuda.synchronize()
         lib.rae_debug_stamps(eng.plan, C.c_void_p(bu.data_ptr()), 0)
-        lib.rae_step_update(eng.plan, it, st)
+        lib.rae_step_update_at(eng.plan, 20 + it, st)
         torch.cuda.synchronize()
         fw.append(bf.cpu().numpy().reshape(gf, 16).astype(np.float64) / 100.0)   # -> us
         up.append(bu.cpu().numpy().reshape(gu * 4, 4).astype(np.float64))
