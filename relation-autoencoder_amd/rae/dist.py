@@ -8,7 +8,7 @@ in-place all-gather (RCCL over xGMI; gloo on CPU) gives every rank all L records
 rank then runs the identical deterministic update, so the replicas stay bit-identical.
 
 This is the same gradient as a dense all-reduce of dW (d,m), dA (n,r), dAb (n), dC (r,m)
-summed over ranks -- at 0.45 MB per rank per step instead of >200 MB for the dense
+summed over ranks -- at 0.52 MB per rank per step instead of >200 MB for the dense
 gradients at the headline shape.
 """
 from __future__ import annotations
