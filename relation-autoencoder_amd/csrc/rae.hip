@@ -84,6 +84,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_dp2(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_gemm_dp2<NJS, MT>(a, blockIdx.x, smem);
 }
+__global__ __launch_bounds__(RAE_BT) void k_bil_prep(StepArgs a) { bil_prep(a); }
 __global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
     __shared__ float sdp[1024];
     __shared__ float red[2 * RAE_NWAVE];
@@ -486,6 +487,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.nib = bil ? (p->dp2 ? (c.embed + RAE_IB2 - 1) / RAE_IB2 : (c.embed + RAE_IB - 1) / RAE_IB) : 0;
     const size_t o_mbuf = bil ? take(4ull * c.batch_size * c.embed * c.embed) : 0;
     const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
+    a.Lp = (L + 31) / 32 * 32;
+    const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
+    const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
     if (e != hipSuccess) {
         delete p;
@@ -509,6 +513,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
     a.Mbuf = bil ? reinterpret_cast<float*>(p->ws + o_mbuf) : nullptr;
     a.dPpart = bil ? reinterpret_cast<float*>(p->ws + o_dpp) : nullptr;
+    a.facT = a.bf16 ? reinterpret_cast<float*>(p->ws + o_fac) : nullptr;
+    a.pfrag = a.bf16 ? reinterpret_cast<uint4*>(p->ws + o_pfr) : nullptr;
     a.err = p->d_err;
     a.cursor = p->d_cursor;
 
@@ -638,6 +644,10 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
 template <int OPT, bool V4, bool BIL>
 static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
     if constexpr (BIL) {
+        if (a.bf16) {
+            const int gp = 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
+            RAE_LAUNCH(p, k_bil_prep, dim3(gp), bt, 0, st, a);
+        }
         if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
         else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
     } else {

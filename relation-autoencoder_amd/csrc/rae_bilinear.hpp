@@ -732,40 +732,95 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
 // ---- update: 16 rows ij of the R/C tensor (viewed as (r*r, m)) against all m columns ------
 // gR[ij][k] = sum_b U_b[ij] P_b[k] over the global batch, then the optimizer in place.
 // A[ij][kk] = U_{b0+kk}[ij], B[kk][k] = P_{b0+kk}[k], D[ij][k].
-// bf16-operand gradient of 16 rows ij x 16 columns per tile: K = examples in steps of 32
+// k_bil_prep: lay out the bf16 R-gradient operands of the global batch (after the exchange).
+// Blocks [0, 4*nit*nbs): one (factor, 64 rows i, 32 examples) tile, read along i (coalesced
+// record runs), transposed through LDS, written along the examples.  The last nbs*nkt
+// blocks: one (32 examples, 16 relations) P tile -> its 64 lanes' B fragments.
+__device__ int bil_prep_blocks(const StepArgs& a) {
+    return 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
+}
+__device__ void bil_prep(const StepArgs& a) {
+    __shared__ float tile[32][65];
+    const int r = a.r, m = a.m, L = a.L, Lp = a.Lp, tid = threadIdx.x;
+    const int nit = (r + 63) / 64, nbs = Lp / 32, nkt = (m + 15) / 16;
+    const int nfacb = 4 * nit * nbs;
+    const int blk = blockIdx.x;
+    if (blk < nfacb) {
+        const int bs = blk % nbs, rest = blk / nbs, it = rest % nit, f = rest / nit;
+        const int off = f == 0 ? a.lay.oX : f == 1 ? a.lay.oA1 : f == 2 ? a.lay.oA2 : a.lay.oY;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int bb = (tid >> 6) + 4 * u, i = it * 64 + (tid & 63), b = bs * 32 + bb;
+            tile[bb][tid & 63] = (b < L && i < r) ? a.ex[(int64_t)b * a.lay.rec + off + i] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int ii = (tid >> 5) + 8 * u, bb = tid & 31, i = it * 64 + ii;
+            if (i < r) a.facT[((int64_t)f * r + i) * Lp + bs * 32 + bb] = tile[bb][ii];
+        }
+    } else if (blk < nfacb + nbs * nkt) {
+        const int t = blk - nfacb, bs = t / nkt, kt = t - bs * nkt;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int bb = (tid >> 4) + 16 * u, k = kt * 16 + (tid & 15), b = bs * 32 + bb;
+            tile[bb][tid & 15] = (b < L && k < m) ? a.ex[(int64_t)b * a.lay.rec + a.lay.oP + k] : 0.f;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const int g = tid >> 4, li = tid & 15;
+            rae_bf16x8 v;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = (__bf16)tile[8 * g + q][li];
+            a.pfrag[(int64_t)t * 64 + tid] = *reinterpret_cast<const uint4*>(&v);
+        }
+    }
+}
+
+// bf16-operand gradient of 16 rows ij x 16 columns per tile: K = examples in steps of 32.
+// The lane's 8 examples' factors are two float4 loads per factor (k_bil_prep's transposed
+// copies) and each P fragment one 16-byte load.
 __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ijt, int kg0, int nk,
                                                        rae_bf4* acc, int lane) {
-    const int m = a.m, r = a.r, L = a.L;
+    const int r = a.r, L = a.L, Lp = a.Lp, nkt = (a.m + 15) / 16;
     const int64_t rr = (int64_t)r * r;
     const int li = lane & 15, g = lane >> 4;
     const int64_t ij = (int64_t)ijt * 16 + li;
     const bool ijv = ij < rr;
     const int ijc = (int)(ijv ? ij : 0);
     const int i = ijc / r, j = ijc - (ijc / r) * r;
+    const float* xt = a.facT + (int64_t)i * Lp;
+    const float* a1t = a.facT + (int64_t)(r + i) * Lp;
+    const float* a2t = a.facT + (int64_t)(2 * r + j) * Lp;
+    const float* yt = a.facT + (int64_t)(3 * r + j) * Lp;
     for (int b0 = 0; b0 < L; b0 += 32) {
+        const int bb = b0 + 8 * g;
+        float xv[8], a1v[8], a2v[8], yv[8];
+        *reinterpret_cast<float4*>(xv) = *reinterpret_cast<const float4*>(xt + bb);
+        *reinterpret_cast<float4*>(xv + 4) = *reinterpret_cast<const float4*>(xt + bb + 4);
+        *reinterpret_cast<float4*>(a1v) = *reinterpret_cast<const float4*>(a1t + bb);
+        *reinterpret_cast<float4*>(a1v + 4) = *reinterpret_cast<const float4*>(a1t + bb + 4);
+        *reinterpret_cast<float4*>(a2v) = *reinterpret_cast<const float4*>(a2t + bb);
+        *reinterpret_cast<float4*>(a2v + 4) = *reinterpret_cast<const float4*>(a2t + bb + 4);
+        *reinterpret_cast<float4*>(yv) = *reinterpret_cast<const float4*>(yt + bb);
+        *reinterpret_cast<float4*>(yv + 4) = *reinterpret_cast<const float4*>(yt + bb + 4);
+        rae_bf16x8 pb[RAE_KG];
+        const uint4* pf = a.pfrag + ((int64_t)(b0 / 32) * nkt + kg0) * 64 + lane;
+#pragma unroll
+        for (int q = 0; q < RAE_KG; ++q) {
+            const uint4 u = pf[(q < nk ? q : 0) * 64];
+            pb[q] = *reinterpret_cast<const rae_bf16x8*>(&u);
+        }
         rae_bf16x8 ua;
-        const float* erb[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int b = b0 + 8 * g + e;
-            const bool bv = b < L;
-            const float* er = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec;
-            erb[e] = er;
-            const float u = er[a.lay.oX + i] * er[a.lay.oA2 + j] + er[a.lay.oA1 + i] * er[a.lay.oY + j];
-            ua[e] = (__bf16)((bv && ijv) ? u : 0.f);
+            const float u = xv[e] * a2v[e] + a1v[e] * yv[e];    // zero past L (padded factors)
+            ua[e] = (__bf16)(ijv ? u : 0.f);
         }
 #pragma unroll
         for (int q = 0; q < RAE_KG; ++q) {
             if (q >= nk) continue;
-            const int k = (kg0 + q) * 16 + li;
-            const bool kv = k < m;
-            rae_bf16x8 pb;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const bool bv = b0 + 8 * g + e < L;
-                pb[e] = (__bf16)((bv && kv) ? erb[e][a.lay.oP + (kv ? k : 0)] : 0.f);
-            }
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, pb, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, pb[q], acc[q], 0, 0, 0);
         }
     }
 }

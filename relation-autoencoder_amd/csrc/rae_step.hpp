@@ -93,6 +93,12 @@ struct StepArgs {
     float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
     int nib;             // bilinear: number of i-blocks of the dP contraction
     int bf16;            // bilinear: bf16 MFMA operands (fp32 accumulation) for the R GEMMs
+    // bf16 R-gradient operands laid out by k_bil_prep after the exchange: the rank-2 factors
+    // X, A1, A2, Y of the global batch transposed to (4, r, Lp) fp32 (example-minor, Lp = L
+    // rounded up to 32, zero padded) and P as ready B fragments (L/32, K/16, 64 lanes) x 8 bf16
+    float* facT;
+    uint4* pfrag;
+    int Lp;
     double* regpart;     // [nreg][2] L1/L2 partials of regularised rows
     int nregC;           // number of decoder-row partial slots
     int nregW;           // number of dense-W block partial slots
