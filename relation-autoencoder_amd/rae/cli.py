@@ -5,9 +5,9 @@ defaults and meaning), plus the README's aliases (README.md:44: --pickled_datase
 
     python -m rae DATASET --model-name NAME --decoder sp [--epochs 100 ...]
 
-DATASET is a dataset written by rae.data.save_npz (the reference's Py2 pickles from
-processing/OiePreprocessor.py are out of scope), or ``synthetic:N[:d[:K]]`` for the SURVEY 8(d)
-generator.  Multi-GPU: launch with torch.distributed.run, one process per GPU.
+DATASET is a preprocessed file written by ``python -m rae.preprocess`` (.json / .json.gz: the
+reference's OiePreprocessor output, stored without pickles), an array dataset written by
+rae.data.save_npz, or ``synthetic:N[:d[:K]]`` for the SURVEY 8(d) generator.  Multi-GPU: launch with torch.distributed.run, one process per GPU.
 """
 from __future__ import annotations
 
@@ -29,7 +29,8 @@ def get_command_args(argv=None, program_name="rae"):
                                 description="Trains a basic Open Information Extraction Model",
                                 formatter_class=argparse.ArgumentDefaultsHelpFormatter)
     p.add_argument("dataset", nargs="?", default=None,
-                   help="dataset .npz (rae.data.save_npz) or synthetic:N[:d[:K]]")
+                   help="preprocessed .json[.gz] (rae.preprocess), dataset .npz "
+                        "(rae.data.save_npz) or synthetic:N[:d[:K]]")
     p.add_argument("--pickled_dataset", dest="dataset_alias", default=None, help=argparse.SUPPRESS)
     p.add_argument("--epochs", type=int, default=100, help="the number of training epochs")
     p.add_argument("--learning-rate", "--learning_rate", dest="learning_rate", type=float,
@@ -95,6 +96,9 @@ def load_dataset(spec: str, seed: int = 1234):
         d = parts[1] if len(parts) > 1 else 2 ** 17
         K = parts[2] if len(parts) > 2 else 10
         return synthetic_dataset(N, d, K, seed=seed)
+    if spec.endswith((".json", ".json.gz")):
+        from .preprocess import load_data
+        return load_data(spec)
     return load_npz(spec)
 
 

@@ -325,3 +325,41 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
         a, b = out[0][0][k], out[1][0][k]
         rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
         assert rel < 1e-4, f"{k}: relative distance {rel:.3e}"
+
+
+@pytest.mark.parametrize("dec,m,hp", [
+    ("sp", 10, dict(l2=0.1, alpha=0.1)),          # README.md:44 (C1: K=10, embed 10, neg 5, l=100)
+    ("rescal+sp", 5, dict(l2=0.1, alpha=0.1)),    # test.py:33 (2 epochs, rescal+sp, 5 relations)
+])
+def test_c1_data_sample_vs_oracle(built_lib, cuda_dev, dec, m, hp):
+    """BASELINE config 1: data-sample.txt ingested by rae.preprocess (fixture c1_sample.npz,
+    oracle/gen_c1_fixture.py) trained on the GPU, against the float64 oracle on the same
+    seed; relation assignments identical where the margin is clear; B^3 on the gold labels."""
+    from rae.data import load_npz
+    from rae.evaluation import construct_split_evaluator
+    from rae.inducer import ReconstructInducer
+    data, gold = load_npz(os.path.join(GOLDEN, "c1_sample.npz"))
+    r, s, l, ep = 10, 5, 100, 2
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), ep, 0.1, l, r, m, s, 0.0,
+                             hp["l2"], "adagrad", "c1", dec, False, True, False, hp["alpha"],
+                             device=cuda_dev, graph_chunk=4)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=hp["alpha"],
+                                   lambda2=hp["l2"])
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "c1")
+    lab = ind.func["label_train"].all_labels(ind.batch_reps["train"])
+    want, _ = tr.labels()
+    X = data.split["train"].xFeats
+    S = np.asarray(X @ tr.params["W"]) + tr.params["Wb"]
+    srt = np.sort(S, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-5
+    assert clear.mean() > 0.9
+    assert np.array_equal(lab[clear], want[clear])
+    f = []
+    for labels in (lab, want):
+        ev = construct_split_evaluator(gold["train"], "train")
+        ev.feed_induced_clusters({i: set(np.flatnonzero(labels == i).tolist()) for i in range(m)})
+        f.append(ev.compute_metrics())
+    if np.array_equal(lab, want):
+        assert f[0] == f[1]
