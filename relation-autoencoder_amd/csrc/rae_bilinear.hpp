@@ -34,6 +34,9 @@ namespace rae {
 typedef float rae_bf4 __attribute__((ext_vector_type(4)));
 #define RAE_IB 8     // i rows per dP partial block (k_bil_dp)
 #define RAE_KG 8     // 16-column tiles of m per pass of one R-row task (task_bilinear_rows)
+#ifndef RAE_SWEEP_RB
+#define RAE_SWEEP_RB 4   // M_b rows per wave whose loads are in flight together (bil_sweep)
+#endif
 
 // ---- k_bil_enc: encoder + hybrid SP projections --------------------------------------------
 template <bool V4>
@@ -440,7 +443,7 @@ __device__ void bil_sweep(const float* M, int r, const float* vr, const float* v
                           float* col_out, float* part) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
-    constexpr int RB = 4;
+    constexpr int RB = RAE_SWEEP_RB;
     const int rv = r / VW, r4 = align4(r);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const VT* vrv = reinterpret_cast<const VT*>(vr);
