@@ -514,6 +514,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     (void)m;
+    RAE_STAMP(a, 0);
 
     if (threadIdx.x < NJ) {
         const int j = threadIdx.x;
@@ -534,6 +535,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     }
     const float H = rec[a.lay.oloss];
     __syncthreads();
+    RAE_STAMP(a, 1);
     // negative rows: rows[t] = A[n1_t], rows[s + t] = A[n2_t]
     for (int e = threadIdx.x; e < 2 * s * rv; e += RAE_FBT) {
         const int t = e / rv, c = e - t * rv;
@@ -542,6 +544,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     }
     const float* Mb = a.Mbuf + (int64_t)bl * r * r;
     bil_sweep<V4>(Mb, r, S.a2, S.a1, S.v, S.w, S.part);     // v = M a2, w = M^T a1 (+ barrier)
+    RAE_STAMP(a, 2);
 
     // dot products: rho < s: n1_t.(v [+ wC1]); s <= rho < 2s: n2_t.(w [+ wC2]);
     // 2s: a1.v; 2s+1: a1.wC1; 2s+2: a2.wC2
@@ -574,6 +577,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         }
     }
     __syncthreads();
+    RAE_STAMP(a, 3);
 
     // scores, loss, coefficients (wave 0)
     if (w == 0) {
@@ -629,7 +633,9 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         }
     }
     __syncthreads();
+    RAE_STAMP(a, 4);
     bil_sweep<V4>(Mb, r, S.y, S.x, S.My, S.Mtx, S.part);    // M y, M^T x
+    RAE_STAMP(a, 5);
 
     {
         const float dOne = S.red[0], ca1 = S.red[1], ca2 = S.red[2];
@@ -651,6 +657,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         }
         if (threadIdx.x == 0) rec[a.lay.oloss] = S.red[32];
     }
+    RAE_STAMP(a, 6);
 }
 
 // ---- k_bil_dp: dP partials of one (16 examples) x (16 relations) tile over RAE_IB rows i ----

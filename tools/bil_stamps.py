@@ -1,0 +1,69 @@
+"""Phase timing of k_bil_dec (the RESCAL decoder's per-example kernel) from in-kernel
+s_memrealtime stamps (100 MHz), on a bilinear BASELINE config (default C5).  Uses the
+diagnostic library of tools/phase_stamps.py (-DRAE_STAMPS).  Diagnostic only.
+
+    python tools/bil_stamps.py [--config c5] [--iters 10]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import phase_stamps as PS  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c5")
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    PS.build_diag()
+    os.environ["RAE_LIB"] = PS.DIAG
+    import torch
+    import bench
+    from rae import _lib
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    lib = _lib.load()
+    lib.rae_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    lib.rae_debug_grid.argtypes = [C.c_void_p, C.c_void_p]
+    cfg = bench.CONFIGS[args.config]
+    dev = torch.device("cuda", 0)
+    data, gold = synthetic_dataset(cfg["N"], cfg["d"], cfg["ntrue"], seed=1234)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 100, cfg["r"], cfg["m"],
+                             cfg["s"], 0.0, 0.0, "adagrad", "stamps", cfg["dec"], False, True, False,
+                             1.0, device=dev, graph_chunk=1, mfma_bf16=cfg.get("bf16", False))
+    ind.compile_function()
+    eng = ind.engine
+    n1, n2 = ind.draw_epoch_negatives()
+    eng.set_epoch_negatives(n1, n2)
+    eng.run(0, 20, graph=False)
+    torch.cuda.synchronize()
+    grid = (C.c_int * 4)()
+    lib.rae_debug_grid(eng.plan, grid)
+    gf = list(grid)[0]
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.rae_build_index(eng.plan, 20, args.iters, st)
+    per = []
+    for it in range(args.iters):
+        bf = torch.zeros(gf * 16, dtype=torch.int64, device=dev)
+        lib.rae_debug_stamps(eng.plan, C.c_void_p(bf.data_ptr()), 1)
+        lib.rae_step_forward_at(eng.plan, 20 + it, st)
+        lib.rae_debug_stamps(eng.plan, None, 1)
+        lib.rae_step_update_at(eng.plan, 20 + it, st)
+        torch.cuda.synchronize()
+        f = bf.cpu().numpy().reshape(gf, 16).astype(np.float64)[:, :7] / 100.0   # -> us
+        t0 = f[:, 0].min()
+        per.append(np.concatenate([f[:, :1] - t0, np.diff(f, axis=1), f[:, -1:] - t0], axis=1))
+    per = np.concatenate(per)
+    cols = ["start", "ids+rec", "sweep1", "negrows+dots", "coef+xy", "sweep2", "record", "end"]
+    print(f"k_bil_dec ({args.config}, {gf} workgroups), median/max us per phase:")
+    print("  " + "  ".join(f"{c} {np.median(per[:, i]):.2f}/{per[:, i].max():.2f}"
+                           for i, c in enumerate(cols)))
+
+
+if __name__ == "__main__":
+    main()
