@@ -59,8 +59,12 @@ __global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* __restrict__ in
                 for (int u = 0; u < U; ++u) {
                     const int t = t0 + u * RPW + grp;
                     const int tc = t < nf ? t : 0;
+                    // both shuffles run on every lane: a ds_bpermute inside the t < nf branch
+                    // reads source lanes that are inactive there (garbage), which dropped the
+                    // last feature of rows with nnz = 17, 33, ... (LPR = 16 / 32)
                     const int f = __shfl(fid, tc, 64);
-                    v[u] = t < nf ? __shfl(fval, tc, 64) : 0.f;
+                    const float fv = __shfl(fval, tc, 64);
+                    v[u] = t < nf ? fv : 0.f;
                     const VT* row = Wv + (int64_t)f * mv;
                     x[u][0] = row[col < mv ? col : 0];
                     if (NQ > 1) x[u][1] = row[col + 64 < mv ? col + 64 : 0];

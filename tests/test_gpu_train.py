@@ -363,3 +363,90 @@ def test_c1_data_sample_vs_oracle(built_lib, cuda_dev, dec, m, hp):
         f.append(ev.compute_metrics())
     if np.array_equal(lab, want):
         assert f[0] == f[1]
+
+
+def _edge_dataset(seed=11):
+    """Ragged inputs the reference accepts: examples with no features (every feature of the
+    example thresholded away, OiePreprocessor.py:200-208 -> an empty CSR row), examples longer
+    than the fast path's descriptor (general path), e1 == e2, negatives equal to the positive
+    entities (Zipf-heavy CDF), and N not a multiple of l (tail dropped, OieInduction.py:98)."""
+    from rae.data import DatasetManager
+    g = np.random.RandomState(seed)
+    N, d, n = 530, 900, 25
+    lens = g.randint(1, 20, size=N)
+    lens[::17] = 0                                   # empty rows
+    lens[5::97] = 300                                # longer than the descriptor capacity
+    rows = np.repeat(np.arange(N), lens)
+    cols = np.concatenate([g.choice(d, size=k, replace=False) for k in lens])
+    X = sp.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(N, d))
+    a1 = (g.zipf(1.6, N) % n).astype(np.int32)
+    a2 = (g.zipf(1.6, N) % n).astype(np.int32)
+    a2[::7] = a1[::7]                                # e1 == e2
+    a1[:n] = np.arange(n)
+    return DatasetManager.from_arrays(X, a1, a2, n_entities=n)
+
+
+@pytest.mark.parametrize("dec", ["sp", "rescal+sp"])
+def test_ragged_inputs_vs_oracle(built_lib, cuda_dev, dec):
+    from rae.inducer import ReconstructInducer
+    data = _edge_dataset()
+    X = data.split["train"].xFeats
+    assert np.diff(X.indptr).min() == 0 and np.diff(X.indptr).max() == 300
+    m, r, s, l, ep = 12, 16, 4, 100, 2
+    ind = ReconstructInducer(data, {"train": {}}, np.random.RandomState(2), ep, 0.1, l, r, m, s,
+                             0.0, 0.0, "adagrad", "edge", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2)
+    ind.learn(verbose=False)
+    assert ind.batch_reps["train"] == 5                         # 530 // 100, tail dropped
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "ragged")
+    lab = ind.func["label_train"].all_labels(ind.batch_reps["train"])
+    want, _ = tr.labels()
+    # the labelling kernel is the argmax of the trained (device) parameters; against the
+    # float64 trajectory the labels agree except at near-ties within the parameter tolerance
+    got = _params(ind)
+    S = np.asarray(X[:len(want)] @ got["W"]) + got["Wb"]
+    srt = np.sort(S, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert np.array_equal(lab[clear], np.argmax(S, axis=1)[clear])
+    assert np.mean(lab == want) > 0.97
+    # empty rows score Wb alone: one shared label
+    empty = np.flatnonzero(np.diff(X.indptr)[:len(want)] == 0)
+    assert len(set(lab[empty].tolist())) == 1
+
+
+@pytest.mark.parametrize("m", [12, 100, 300, 7])      # 16 / 32 / 64 lanes per row; scalar path
+def test_label_pass_every_row_length(built_lib, cuda_dev, m):
+    """rae_label on rows of every length 0..130 (each length ten times): the lane-group
+    gather's partial last rounds (nnz = 17, 33, ... once dropped a feature) and the
+    64-feature chunking, against the float64 oracle's probabilities and labels."""
+    import ctypes as C
+    import torch
+    from rae import _lib
+    from rae.engine import DeviceSplit
+    from rae.data import DatasetSplit
+    g = np.random.RandomState(m)
+    d = 4000
+    lens = np.repeat(np.arange(131), 10)
+    rows = np.repeat(np.arange(len(lens)), lens)
+    cols = np.concatenate([g.choice(d, size=k, replace=False) for k in lens])
+    X = sp.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(len(lens), d))
+    n = X.shape[0]
+    split = DeviceSplit(DatasetSplit(np.zeros(n, np.int32), np.zeros(n, np.int32), X), cuda_dev)
+    W = g.standard_normal((d, m)).astype(np.float32)
+    Wb = g.standard_normal(m).astype(np.float32)
+    lab = torch.empty(n, dtype=torch.int64, device=cuda_dev)
+    pr = torch.empty((n, m), dtype=torch.float32, device=cuda_dev)
+    lib = _lib.load()
+    Wt, Wbt = torch.as_tensor(W, device=cuda_dev), torch.as_tensor(Wb, device=cuda_dev)
+    _lib.check(lib.rae_label(C.c_void_p(split.indptr.data_ptr()), C.c_void_p(split.indices.data_ptr()),
+                             None, C.c_void_p(Wt.data_ptr()), C.c_void_p(Wbt.data_ptr()), m, 0, n,
+                             C.c_void_p(lab.data_ptr()), C.c_void_p(pr.data_ptr()), None))
+    torch.cuda.synchronize()
+    want_lab, want_p = O.label(X, W.astype(np.float64), Wb.astype(np.float64))
+    np.testing.assert_allclose(pr.cpu().numpy(), want_p, rtol=1e-4, atol=1e-6)
+    S = np.asarray(X @ W.astype(np.float64)) + Wb
+    srt = np.sort(S, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert np.array_equal(lab.cpu().numpy()[clear], want_lab[clear])
