@@ -450,3 +450,23 @@ def test_label_pass_every_row_length(built_lib, cuda_dev, m):
     srt = np.sort(S, axis=1)
     clear = (srt[:, -1] - srt[:, -2]) > 1e-4
     assert np.array_equal(lab.cpu().numpy()[clear], want_lab[clear])
+
+
+@pytest.mark.parametrize("dec", ["sp", "rescal", "rescal+sp"])
+@pytest.mark.parametrize("shape", [(1, 4, 1, 1), (3, 1, 1, 3), (2, 5, 2, 7), (17, 3, 1, 5)],
+                         ids=["m1_l1", "r1", "odd", "m17"])
+def test_degenerate_shapes_vs_oracle(built_lib, cuda_dev, dec, shape):
+    """Smallest shapes the reference's constructor accepts: one relation, one-dimensional
+    embeddings, a single negative, a batch of one example (K = 1 MFMA chains, scalar
+    paths, partial tiles everywhere)."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = shape
+    data, gold = synthetic_dataset(60, 300, 3, seed=21)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "tiny", dec, False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=2)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, 1, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "tiny")
