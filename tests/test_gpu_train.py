@@ -470,3 +470,31 @@ def test_degenerate_shapes_vs_oracle(built_lib, cuda_dev, dec, shape):
     tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, 1, lr=0.1, alpha=1.0)
     np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
     _assert_params_close(_params(ind), tr.params, "tiny")
+
+
+@pytest.mark.parametrize("dec", ["sp", "rescal+sp"])
+def test_hot_rows_vs_oracle(built_lib, cuda_dev, dec):
+    """Collisions at their worst: five entities, every e1 the same entity, one feature in every
+    example -- a single A row and a single W row receive hundreds of contributions per step
+    (the update's multi-chunk record loops and wide rounds)."""
+    from rae.data import DatasetManager
+    from rae.inducer import ReconstructInducer
+    g = np.random.RandomState(3)
+    N, d, n = 400, 50, 5
+    lens = g.randint(1, 6, size=N)
+    rows = np.repeat(np.arange(N), lens + 1)
+    cols = np.concatenate([np.concatenate([[0], 1 + g.choice(d - 1, size=k, replace=False)])
+                           for k in lens])
+    X = sp.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(N, d))
+    a1 = np.zeros(N, np.int32)
+    a2 = g.randint(0, n, N).astype(np.int32)
+    a2[:n] = np.arange(n)
+    data = DatasetManager.from_arrays(X, a1, a2, n_entities=n)
+    m, r, s, l, ep = 8, 16, 4, 100, 2
+    ind = ReconstructInducer(data, {"train": {}}, np.random.RandomState(2), ep, 0.1, l, r, m, s,
+                             0.0, 0.0, "adagrad", "hot", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "hot")
