@@ -5,7 +5,9 @@
 
 #define RAE_WAVE 64
 #define RAE_FBT 512           // threads per workgroup of the forward kernel (8 waves)
+#ifndef RAE_BT
 #define RAE_BT 256            // threads per workgroup of the update kernels (4 waves)
+#endif
 #define RAE_NWAVE (RAE_BT / RAE_WAVE)
 #define RAE_KCAP 8192         // LDS capacity (64-bit keys) of one row-index partition
 #define RAE_PART 256          // target records per row-index partition
