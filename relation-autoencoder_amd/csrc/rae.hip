@@ -65,7 +65,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_m(StepArgs a) {
     else bil_gemm_m<V4>(a, t, threadIdx.x & 63);
 }
 template <bool V4>
-__global__ __launch_bounds__(RAE_FBT) void k_bil_dec(StepArgs a) {
+__global__ __launch_bounds__(RAE_DBT) void k_bil_dec(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_decode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
@@ -613,7 +613,7 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
         RAE_LAUNCH(p, (k_bil_m<V4, true>), dim3(gm), dim3(RAE_BT), 0, st, a);
     else
         RAE_LAUNCH(p, (k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
-    RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_FBT), p->smem_dec, st, a);
+    RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
     const size_t lds77 = dp2_lds_bytes<7, 7>(), lds88 = dp2_lds_bytes<8, 8>();
     if (p->dp2 == 1)

@@ -405,6 +405,12 @@ __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
 }
 
 // ---- k_bil_dec helpers ----------------------------------------------------------------------
+// k_bil_dec runs 16 waves per example (RAE_DBT threads), twice the forward kernels' 8: the two
+// M_b sweeps are bound by how many loads each CU has in flight (C5 forward 79.3 -> 73.8 us)
+#ifndef RAE_DBT
+#define RAE_DBT 1024
+#endif
+#define RAE_DNW (RAE_DBT / RAE_WAVE)
 struct BilSmem {
     float *v, *w, *a1, *a2, *wC1, *wC2, *x, *y, *My, *Mtx, *dw1, *dw2, *rows, *part, *dots, *Abv,
         *coef, *red;
@@ -413,7 +419,7 @@ struct BilSmem {
 
 __host__ __device__ inline int bil_dec_smem_floats(int r, int s) {
     const int r4 = align4(r), NJ4 = align4(2 + 2 * s);
-    return 12 * r4 + 2 * s * r4 + RAE_FNW * r4 + align4(2 * s + 4) + NJ4 + align4(3 * (2 + 2 * s)) +
+    return 12 * r4 + 2 * s * r4 + RAE_DNW * r4 + align4(2 * s + 4) + NJ4 + align4(3 * (2 + 2 * s)) +
            64 + NJ4;
 }
 
@@ -425,7 +431,7 @@ __device__ inline BilSmem carve_bil_smem(char* smem, int r, int s) {
                         &S.dw1, &S.dw2};
     for (int q = 0; q < 12; ++q) { *vecs[q] = p; p += r4; }
     S.rows = p; p += 2 * s * r4;
-    S.part = p; p += RAE_FNW * r4;
+    S.part = p; p += RAE_DNW * r4;
     S.dots = p; p += align4(2 * s + 4);
     S.Abv = p; p += NJ4;
     S.coef = p; p += align4(3 * (2 + 2 * s));
@@ -454,11 +460,11 @@ __device__ void bil_sweep(const float* M, int r, const float* vr, const float* v
         const int c = lane + 64 * q;
         if (c < rv) vrc[q] = vrv[c]; else vzero(vrc[q]);
     }
-    for (int i0 = w; i0 < r; i0 += RAE_FNW * RB) {
+    for (int i0 = w; i0 < r; i0 += RAE_DNW * RB) {
         VT x[RB][2];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-            const int i = min(i0 + RAE_FNW * u, r - 1);
+            const int i = min(i0 + RAE_DNW * u, r - 1);
             const VT* Mi = reinterpret_cast<const VT*>(M + (int64_t)i * r);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -468,7 +474,7 @@ __device__ void bil_sweep(const float* M, int r, const float* vr, const float* v
         }
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-            const int i = i0 + RAE_FNW * u;
+            const int i = i0 + RAE_DNW * u;
             const bool iv = i < r;
             const float li = iv ? vl[i] : 0.f;
             float d = 0.f;
@@ -490,10 +496,10 @@ __device__ void bil_sweep(const float* M, int r, const float* vr, const float* v
         if (c < rv) reinterpret_cast<VT*>(part + w * r4)[c] = cacc[q];
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < r; j += RAE_FBT) {
+    for (int j = threadIdx.x; j < r; j += RAE_DBT) {
         float t = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < RAE_FNW; ++ww) t += part[ww * r4 + j];
+        for (int ww = 0; ww < RAE_DNW; ++ww) t += part[ww * r4 + j];
         col_out[j] = t;
     }
     __syncthreads();
@@ -526,7 +532,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         S.ids[j] = id;
         S.Abv[j] = a.Ab[id];
     }
-    for (int i = threadIdx.x; i < r4; i += RAE_FBT) {
+    for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
         const bool iv = i < r;
         S.a1[i] = iv ? rec[a.lay.oA1 + i] : 0.f;
         S.a2[i] = iv ? rec[a.lay.oA2 + i] : 0.f;
@@ -537,7 +543,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     __syncthreads();
     RAE_STAMP(a, 1);
     // negative rows: rows[t] = A[n1_t], rows[s + t] = A[n2_t]
-    for (int e = threadIdx.x; e < 2 * s * rv; e += RAE_FBT) {
+    for (int e = threadIdx.x; e < 2 * s * rv; e += RAE_DBT) {
         const int t = e / rv, c = e - t * rv;
         const VT* src = reinterpret_cast<const VT*>(a.A + (int64_t)S.ids[2 + t] * r);
         reinterpret_cast<VT*>(S.rows)[t * r4v + c] = src[c];
@@ -557,7 +563,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         const VT* A1 = reinterpret_cast<const VT*>(S.a1);
         const VT* A2 = reinterpret_cast<const VT*>(S.a2);
         const int ntask = 2 * s + 3;
-        for (int rho = w; rho < ntask; rho += RAE_FNW) {
+        for (int rho = w; rho < ntask; rho += RAE_DNW) {
             const VT* xa;
             const VT* xb;
             const VT* xc = nullptr;
@@ -619,7 +625,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     // x = dOne a1 + sum_t dg1_t n1_t ; y = sum_t dg2_t n2_t ; hybrid dw1/dw2 (sums in t order)
     {
         const float dOne = S.red[0], ca1 = S.red[1], ca2 = S.red[2];
-        for (int i = threadIdx.x; i < r4; i += RAE_FBT) {
+        for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
             float n1 = 0.f, n2 = 0.f;
             for (int t = 0; t < s; ++t) {
                 n1 += S.coef[3 * (2 + t)] * S.rows[t * r4 + i];
@@ -639,7 +645,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
 
     {
         const float dOne = S.red[0], ca1 = S.red[1], ca2 = S.red[2];
-        for (int i = threadIdx.x; i < r; i += RAE_FBT) {
+        for (int i = threadIdx.x; i < r; i += RAE_DBT) {
             const float c1 = hybrid ? S.wC1[i] : 0.f, c2 = hybrid ? S.wC2[i] : 0.f;
             rec[a.lay.oV1 + i] = S.v[i] + c1;
             rec[a.lay.oV2 + i] = S.w[i] + c2;
@@ -650,7 +656,7 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
             rec[a.lay.odw1 + i] = hybrid ? S.dw1[i] : 0.f;
             rec[a.lay.odw2 + i] = hybrid ? S.dw2[i] : 0.f;
         }
-        for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
+        for (int j = threadIdx.x; j < NJ; j += RAE_DBT) {
             const float* c = S.coef + 3 * j;
             rec[a.lay.ocoef + 2 * j] = j < 2 ? 1.f : (j < 2 + s ? c[0] : c[1]);
             rec[a.lay.ocoef + 2 * j + 1] = c[2];

@@ -320,7 +320,8 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
                                  device=cuda_dev, graph_chunk=2, mfma_bf16=True)
         ind.learn(verbose=False)
         out.append((_params(ind), np.array(ind.epoch_costs)))
-    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-5)
+    # costs near zero: the two summation orders drift by ~1e-6 absolute over the epoch
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-5, atol=2e-6)
     for k in out[0][0]:
         a, b = out[0][0][k], out[1][0][k]
         rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
