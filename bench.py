@@ -185,7 +185,9 @@ def main():
 
     graphed = args.graph_chunk > 1
     try:
-        eng.run(0, W)                      # includes graph capture
+        if graphed:                        # capture before the warm-up: never inside the timed
+            eng.capture(args.graph_chunk)  # region, whatever --graph-chunk and --warmup are
+        eng.run(0, W)
     except RuntimeError as e:              # e.g. a collective the runtime cannot capture
         if ws == 1 or not graphed:
             raise

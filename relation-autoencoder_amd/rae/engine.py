@@ -232,6 +232,11 @@ class TrainEngine:
             self._graphs[count] = g
         return g
 
+    def capture(self, count: int | None = None):
+        """Capture the HIP graph of ``count`` steps (default: graph_chunk) without running it."""
+        self._ensure_epoch_mode()
+        self._graph(int(count or self.graph_chunk))
+
     def run(self, first_batch: int, count: int, graph: bool = True):
         """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
         negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
