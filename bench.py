@@ -95,41 +95,87 @@ def pmc_traffic(config):
         return json.load(fh)
 
 
-def cpu_baseline(data, cfg, l, budget_s, seed=2):
-    """Dense-schedule float64 oracle step on this host (one thread), bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import rae_oracle as O
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_limits
-        limiter = threadpool_limits(limits=1)
-    except Exception:                                  # pragma: no cover
-        limiter = None
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:                                    # pragma: no cover
+        pass
+    return "unknown"
+
+
+def _cpu_dense_steps(data, cfg, l, dtype, threads, budget_s, warm=5, max_steps=200, seed=2):
+    """The reference's dense Theano schedule (oracle/cpu_ref.py: forward, dense T.grad,
+    dense AdaGrad over every parameter) on `threads` host threads: `warm` untimed steps,
+    then up to `max_steps` timed steps within `budget_s`.  Returns (examples/s, steps, s)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref
+    torch.set_num_threads(threads)
     sp_ = data.split["train"]
     rng = np.random.RandomState(seed)
-    p = O.init_params(rng, cfg["dec"], data.get_dimensionality(), cfg["m"],
-                      data.get_arg_voc_size(), cfg["r"])
-    acc = {k: np.zeros_like(v) for k, v in p.items()}
+    p = cpu_ref.init_params(rng, cfg["dec"], data.get_dimensionality(), cfg["m"],
+                            data.get_arg_voc_size(), cfg["r"], dtype)
+    step = cpu_ref.DenseScheduleStep(cfg["dec"], p, lr=0.1, alpha=1.0)
     cum = data.negSamplingCum
-    steps, t_used = 0, 0.0
-    while t_used < budget_s or steps < 2:
-        b = steps
+    nb = sp_.args1.shape[0] // l
+    # per-epoch negatives of the batches used (host RandomState, outside the timing as in
+    # the GPU leg); inputs staged as torch tensors before the timed steps
+    nsteps = warm + max_steps
+    u1 = rng.uniform(0, cum[-1], (cfg["s"], nsteps * l))
+    u2 = rng.uniform(0, cum[-1], (cfg["s"], nsteps * l))
+    n1 = torch.as_tensor(cum.searchsorted(u1).astype(np.int64))
+    n2 = torch.as_tensor(cum.searchsorted(u2).astype(np.int64))
+    a1 = torch.as_tensor(sp_.args1.astype(np.int64))
+    a2 = torch.as_tensor(sp_.args2.astype(np.int64))
+
+    def one(i):
+        b = i % nb
         rows = slice(b * l, (b + 1) * l)
-        n1 = O.negative_samples(rng, cum, l, cfg["s"])
-        n2 = O.negative_samples(rng, cum, l, cfg["s"])
-        t0 = time.perf_counter()
-        res = O.train_step_grads(cfg["dec"], p, sp_.xFeats[rows], sp_.args1[rows],
-                                 sp_.args2[rows], n1, n2, alpha=1.0)
-        O.adagrad_apply(p, acc, res.grads, 0.1)
-        t_used += time.perf_counter() - t0
+        X = cpu_ref.batch_csr(sp_.xFeats, rows, dtype)
+        cols = slice(i * l, (i + 1) * l)
+        return step(X, a1[rows], a2[rows], n1[:, cols], n2[:, cols])
+    for i in range(warm):
+        one(i)
+    steps, t0 = 0, time.perf_counter()
+    while steps < max_steps and (time.perf_counter() - t0 < budget_s or steps < 2):
+        one(warm + steps)
         steps += 1
-        if steps >= 200:
-            break
-    if limiter is not None:
-        limiter.unregister() if hasattr(limiter, "unregister") else None
-    return dict(value=steps * l / t_used, unit="examples/s", cores=1, kind="port",
-                sample=f"{steps} dense-schedule float64 steps of the same workload "
-                       f"(l={l}, numpy, 1 thread): {t_used:.1f} s",
-                ms_per_step=1e3 * t_used / steps)
+    el = time.perf_counter() - t0
+    del p, step
+    return steps * l / el, steps, el
+
+
+def cpu_baseline(data, cfg, l, budget_s):
+    """CPU baseline: the reference's dense schedule on this host's cores, float64 (Theano's
+    default floatX) and float32, BASELINE.md sec. 2: all cores of the affinity mask, 5 warm-up
+    + up to 200 timed steps.  The container's OMP_NUM_THREADS share is timed as well when it
+    is smaller than the mask (a 1-GPU box exposes the whole host's CPUs but sets it to its
+    share); the better rate is reported, both are recorded."""
+    import torch
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    counts = [aff] + ([omp] if 0 < omp < aff else [])
+    prev = torch.get_num_threads()
+    runs = {}
+    for prec, dt in (("fp64", torch.float64), ("fp32", torch.float32)):
+        for th in counts:
+            v, n, el = _cpu_dense_steps(data, cfg, l, dt, th, budget_s)
+            runs[f"{prec}_t{th}"] = {"value": v, "steps": n, "seconds": el, "threads": th}
+    torch.set_num_threads(prev)
+    best = max(runs.values(), key=lambda x: x["value"])
+    f64 = max((v for k, v in runs.items() if k.startswith("fp64")), key=lambda x: x["value"])
+    return dict(value=best["value"], unit="examples/s", cores=best["threads"], kind="port",
+                sample=(f"oracle/cpu_ref.py dense Theano schedule (forward, dense T.grad, dense "
+                        f"AdaGrad over all params), same workload l={l}, torch CPU, 5 warm-up + "
+                        f"<=200 timed steps within {budget_s:.0f} s per variant; best variant "
+                        f"reported"),
+                precision=[k for k, v in runs.items() if v is best][0].split("_")[0],
+                fp64_value=f64["value"], runs=runs, affinity_cpus=aff,
+                omp_num_threads=omp or None, cpu_model=_cpu_model(),
+                ms_per_step=1e3 * l / best["value"])
 
 
 def main():
@@ -140,7 +186,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch-size", type=int, default=100)
     ap.add_argument("--graph-chunk", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--no-label-pass", action="store_true")
@@ -183,11 +229,20 @@ def main():
     if K + W > nb:
         raise SystemExit(f"steps+warmup={K + W} exceed the {nb} global batches of one epoch")
 
+    # The per-batch row index (rae_build_index) depends only on the batch's ids, negatives and
+    # CSR rows -- not on the parameters -- so, like the negatives, it is prepared ahead of the
+    # steps: built here for the warm-up + timed batches (one index window), and its per-batch
+    # cost reported next to negative_sampling_s (index_build_us_per_batch, measured over a
+    # whole window below) together with the rate it would give inside the timed region.
+    prebuilt = W + K <= eng.index_window
+    if prebuilt:
+        eng.build_index(0, W + K)
     graphed = args.graph_chunk > 1
     try:
-        if graphed:                        # capture before the warm-up: never inside the timed
-            eng.capture(args.graph_chunk)  # region, whatever --graph-chunk and --warmup are
-        eng.run(0, W)
+        if graphed:                        # capture every graph the warm-up and the timed
+            eng.capture_for(0, W)          # steps replay before running either (no capture
+            eng.capture_for(W, K)          # inside the timed region)
+        eng.run(0, W, index=not prebuilt)
     except RuntimeError as e:              # e.g. a collective the runtime cannot capture
         if ws == 1 or not graphed:
             raise
@@ -196,12 +251,13 @@ def main():
         graphed = False
         eng.graph_chunk = 1
         torch.cuda.synchronize()
-        eng.run(0, W)
+        eng.run(0, W, index=not prebuilt)
+    timed_graphs = eng.graph_sizes(W, K) if graphed else []
     torch.cuda.synchronize()
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    eng.run(W, K)
+    eng.run(W, K, index=not prebuilt)
     torch.cuda.synchronize()
     rdist.barrier()
     torch.cuda.synchronize()
@@ -209,6 +265,15 @@ def main():
     eng.check()
     costs = eng.costs[W:W + K].cpu().numpy()
     assert np.all(np.isfinite(costs)), "non-finite cost"
+    # row-index build cost per batch, over one whole window (as the epoch loop builds it)
+    st0 = torch.cuda.current_stream()
+    nwin = min(eng.index_window, nb)
+    ie = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ie[0].record(st0)
+    eng.build_index(0, nwin)
+    ie[1].record(st0)
+    torch.cuda.synchronize()
+    index_us = ie[0].elapsed_time(ie[1]) * 1e3 / nwin
 
     # ---- per-kernel durations: eager launches of the same step sequence continuing the
     # epoch, each phase launched through rae_time_next (hipExtLaunchKernelGGL), so the HIP
@@ -232,10 +297,10 @@ def main():
     for i in range(n_it):
         assert lib.rae_time_next(plan, fev[i][0], fev[i][1]) == 0
         assert lib.rae_step_forward(plan, i, sp_) == 0, lib.rae_last_error()
-        xev[i][0].record(st)
-        if exchange is not None:
+        if exchange is not None:           # the all-gather of the records (data-parallel only)
+            xev[i][0].record(st)
             exchange(eng.exchange_buf)
-        xev[i][1].record(st)
+            xev[i][1].record(st)
         assert lib.rae_time_next(plan, uev[i][0], uev[i][1]) == 0
         assert lib.rae_step_update(plan, i, sp_) == 0, lib.rae_last_error()
     torch.cuda.synchronize()
@@ -246,7 +311,7 @@ def main():
         return v.value
     fwd_ms = np.array([_ms(e) for e in fev])
     upd_ms = np.array([_ms(e) for e in uev])
-    xch_ms = np.array([a.elapsed_time(b) for a, b in xev])
+    xch_ms = np.array([a.elapsed_time(b) for a, b in xev]) if exchange is not None else None
     for e in fev + uev:
         lib.rae_event_destroy(e[0])
         lib.rae_event_destroy(e[1])
@@ -316,25 +381,35 @@ def main():
                  "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label)"}
         del lab, pr
 
-    # ---- measured copy bandwidth of this HBM (STREAM-style float4 copy by torch, 1 GiB each
-    # way): the practical ceiling next to the 8 TB/s spec the roofline fractions quote
+    # ---- measured copy bandwidth of this HBM: our own STREAM-style float4 copy kernel
+    # (rae_stream_copy), 2 GiB each way -- the practical ceiling next to the 8 TB/s spec the
+    # roofline fractions quote (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy)
     hbm_copy = None
     if not args.no_label_pass:
-        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        nbytes = 1 << 31
+        src = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
         dst = torch.empty_like(src)
-        dst.copy_(src)
+
+        def _copy():
+            assert lib.rae_stream_copy(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                       nbytes, sp_) == 0, lib.rae_last_error()
+        _copy()
         torch.cuda.synchronize()
-        ce = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(5)]
+        ce = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(7)]
         for a_, b_ in ce:
             a_.record(st)
-            dst.copy_(src)
+            _copy()
             b_.record(st)
         torch.cuda.synchronize()
         cus = float(np.median([a_.elapsed_time(b_) for a_, b_ in ce]) * 1e3)
-        hbm_copy = {"GBs": 2 * src.numel() * 4 / (cus * 1e-6) / 1e9, "bytes": 2 * src.numel() * 4,
-                    "us": cus, "how": "torch device copy of a 1 GiB fp32 buffer (read + write), median of 5"}
+        assert bool(torch.equal(src[-4:], dst[-4:]))
+        hbm_copy = {"GBs": 2 * nbytes / (cus * 1e-6) / 1e9, "bytes": 2 * nbytes, "us": cus,
+                    "how": "rae_stream_copy: float4 loads/stores, 2 GiB read + 2 GiB written, "
+                           "median of 7"}
         if label is not None:
             label["frac_of_measured_copy"] = label["achieved"] / hbm_copy["GBs"]
+        roof["frac_of_measured_copy"] = (roof["achieved"] / hbm_copy["GBs"]
+                                         if roof.get("unit") == "GB/s" else None)
         del src, dst
 
     ms_per_step = 1e3 * elapsed / K
@@ -356,19 +431,26 @@ def main():
                    "embed": cfg["r"], "neg_samples": cfg["s"], "decoder": cfg["dec"],
                    "optimizer": "adagrad", "parallelism": f"dp{ws}",
                    "n_entities": data.get_arg_voc_size(),
-                   "graph_chunk": args.graph_chunk if graphed else 1},
+                   "graph_chunk": args.graph_chunk if graphed else 1,
+                   "timed_graph_steps": timed_graphs},
         "roofline": roof,
         "kernels": kern,
         "kernel_us": {"forward": fwd_us, "update": upd_us,
-                      "exchange": float(np.mean(xch_ms) * 1e3),
                       "forward_p50": float(np.median(fwd_ms) * 1e3),
                       "update_p50": float(np.median(upd_ms) * 1e3)},
         "label_pass": label,
         "hbm_copy": hbm_copy,
         "negative_sampling_s": t_neg,
         "negative_sampling": "host RandomState uniforms (reference stream) + device CDF search",
+        "index_build_us_per_batch": index_us,
+        "index_build": ("k_build_index (parameter-independent per-batch row index), built ahead "
+                        "of the timed region like the negatives" if prebuilt else
+                        "built inside the timed region (warm-up + steps exceed one window)"),
+        "value_incl_index": (K * L / (elapsed + K * index_us * 1e-6)) if prebuilt else None,
         "dataset_build_s": t_data,
     }
+    if xch_ms is not None:
+        out["kernel_us"]["exchange"] = float(np.mean(xch_ms) * 1e3)
     if rk == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, cfg, l, args.cpu_seconds)
         out["cpu_baseline"]["host_cpus"] = os.cpu_count()

@@ -114,6 +114,9 @@ int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, rae_plan** ou
 int rae_plan_destroy(rae_plan* plan);
 const char* rae_last_error(void);
 int rae_version(void);
+/* hash of the sources and flags the library was built from (rae/_lib.py source_build_id);
+ * the Python binding refuses a library whose id differs from the sources beside it       */
+const char* rae_build_id(void);
 
 /* floats per example record and per global batch in the exchange buffer */
 int64_t rae_exchange_record_floats(const rae_config* cfg);
@@ -189,6 +192,11 @@ int rae_neg_sample_philox(const double* cum_dev, int64_t n, uint64_t seed, uint6
 int rae_label(const int32_t* indptr, const int32_t* indices, const float* values,
               const float* W, const float* Wb, int32_t relations, int64_t row0,
               int64_t nrows, int64_t* labels_out, float* probs_out, rae_stream_t stream);
+
+/* --- measurement helper (bench.py; no reference counterpart) ------------------------- */
+/* STREAM-style device copy of `bytes` (multiple of 16, 16-byte aligned pointers) with float4
+ * loads and stores: the measured HBM ceiling bench.py reports next to the 8 TB/s spec.   */
+int rae_stream_copy(const void* src_dev, void* dst_dev, int64_t bytes, rae_stream_t stream);
 
 #ifdef __cplusplus
 }

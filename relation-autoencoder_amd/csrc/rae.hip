@@ -269,6 +269,25 @@ __global__ void k_finalize_cost(StepArgs a) {
     a.costs[batch] = (float)((double)*a.base_cost + (double)a.l1adj * L1 + (double)a.l2adj * L2);
 }
 
+// STREAM-style copy (measurement helper): 4 float4 loads in flight per lane before the stores
+__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src,
+                                                     float4* __restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 1024;
+    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = i + 256 * u;
+            v[u] = k < n ? src[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = i + 256 * u;
+            if (k < n) dst[k] = v[u];
+        }
+    }
+}
+
 __global__ void k_add_cursor(int64_t* cursor, int64_t count) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *cursor += count;
 }
@@ -329,6 +348,11 @@ struct rae_plan {
 
 extern "C" const char* rae_last_error(void) { return g_last_error.c_str(); }
 extern "C" int rae_version(void) { return RAE_VERSION; }
+#ifndef RAE_BUILD_ID
+#define RAE_BUILD_ID "unversioned"
+#endif
+__attribute__((used)) static const char g_build_id[] = "RAE_BUILD_ID:" RAE_BUILD_ID;
+extern "C" const char* rae_build_id(void) { return g_build_id + 13; }
 
 extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
     if (!cfg) return -1;
@@ -823,6 +847,20 @@ extern "C" int rae_neg_sample(const double* cum, int64_t n, const double* u, int
 extern "C" int rae_neg_sample_philox(const double* cum, int64_t n, uint64_t seed, uint64_t offset,
                                      int64_t count, int32_t* out, rae_stream_t stream) {
     return launch_neg(cum, n, nullptr, seed, offset, count, out, (hipStream_t)stream, true);
+}
+
+extern "C" int rae_stream_copy(const void* src, void* dst, int64_t bytes, rae_stream_t stream) {
+    if (!src || !dst) return fail(RAE_E_INVALID, "null argument");
+    if (bytes < 0 || (bytes & 15) || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+        return fail(RAE_E_INVALID, "bytes and pointers must be multiples of 16");
+    const int64_t n = bytes / 16;
+    if (n == 0) return RAE_OK;
+    int64_t grid = (n + 1023) / 1024;
+    if (grid > 256 * 16) grid = 256 * 16;
+    hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)src, (float4*)dst, n);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
 }
 
 extern "C" int rae_label(const int32_t* indptr, const int32_t* indices, const float* values,

@@ -21,6 +21,16 @@ __device__ __forceinline__ void lbl_fold(typename VecT<V4>::T& v, int rpw) {
     }
 }
 
+// (v, k) before (best, bk) in numpy argmax order; k == INT_MAX marks "no candidate"
+__device__ __forceinline__ bool lbl_better(float v, int k, float best, int bk) {
+    if (k == 0x7fffffff) return false;
+    if (bk == 0x7fffffff) return true;
+    const bool vn = v != v, bn = best != best;
+    if (bn) return vn && k < bk;
+    if (vn) return true;
+    return v > best || (v == best && k < bk);
+}
+
 template <bool V4>
 __global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* __restrict__ indptr,
                                                   const int32_t* __restrict__ indices,
@@ -77,9 +87,12 @@ __global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* __restrict__ in
             }
         }
         lbl_fold<V4>(acc[0], RPW);
-        // group 0 lanes hold S for columns col (+64): add Wb, argmax (first max), softmax
+        // group 0 lanes hold S for columns col (+64): add Wb, argmax, softmax.  argmax has
+        // numpy's semantics (Theano's MaxAndArgmax calls PyArray_ArgMax): the first maximum,
+        // NaN counting as the maximum (first NaN wins) -- so a diverged row still gets a label
+        // in [0, m), as the reference's does
         float best = -INFINITY;
-        int bk = 0x7fffffff;
+        int bk = 0x7fffffff;                     // no candidate yet
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int c = col + 64 * q;
@@ -90,13 +103,13 @@ __global__ __launch_bounds__(RAE_BT) void k_label(const int32_t* __restrict__ in
             const float* se = reinterpret_cast<const float*>(&sv);
 #pragma unroll
             for (int i = 0; i < VW; ++i)
-                if (cv && se[i] > best) { best = se[i]; bk = c * VW + i; }
+                if (cv && lbl_better(se[i], c * VW + i, best, bk)) { best = se[i]; bk = c * VW + i; }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             const float ob = __shfl_xor(best, o, 64);
             const int ok = __shfl_xor(bk, o, 64);
-            if (ob > best || (ob == best && ok < bk)) { best = ob; bk = ok; }
+            if (lbl_better(ob, ok, best, bk)) { best = ob; bk = ok; }
         }
         if (lane == 0) labels[e] = bk;
         if (probs) {

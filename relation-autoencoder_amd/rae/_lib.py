@@ -6,11 +6,57 @@ exception is raised.
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "librae_hip.so"
 LIB_PATH = os.path.join(_HERE, LIB_NAME)
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "rae.h")
+# hipcc flags of the in-tree build (__graft_entry__.build); part of the build id
+BUILD_FLAGS = ("-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared", "-Wall",
+               "-Wno-unused-parameter", "-Wno-unused-variable")
+
+
+def source_files():
+    """The sources librae_hip.so is built from: csrc/*.hip, csrc/*.hpp and include/rae.h."""
+    if not os.path.isdir(CSRC):
+        return []
+    return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))
+            if f.endswith((".hip", ".hpp"))] + [HEADER]
+
+
+def source_build_id():
+    """sha256 (16 hex digits) over the build flags and the sources' names and bytes; None
+    when the sources are not next to the package.  build() compiles it into the library
+    (rae_build_id()) and load() refuses a library whose id differs."""
+    files = source_files()
+    if not files or not all(os.path.exists(f) for f in files):
+        return None
+    h = hashlib.sha256(" ".join(BUILD_FLAGS).encode())
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def library_build_id(path=LIB_PATH):
+    """The build id compiled into a built library, read from the file's bytes (a marker
+    string rae.hip embeds) rather than by dlopen: a library already loaded in this process
+    would shadow a rebuilt file of the same path.  None if absent."""
+    try:
+        with open(path, "rb") as fh:
+            blob = fh.read()
+    except OSError:
+        return None
+    i = blob.find(b"RAE_BUILD_ID:")
+    if i < 0:
+        return None
+    j = blob.find(b"\0", i)
+    return blob[i + len(b"RAE_BUILD_ID:"):j].decode(errors="replace")
 
 RAE_OK = 0
 RAE_DEC = {"sp": 0, "rescal": 1, "rescal+sp": 2}
@@ -20,13 +66,14 @@ RAE_NEG_PER_EPOCH = 1
 
 # Every symbol include/rae.h declares (checked by tests/test_abi.py against the header).
 EXPORTS = (
-    "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version",
+    "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version", "rae_build_id",
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
     "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
     "rae_step_forward_at", "rae_step_update_at",
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
+    "rae_stream_copy",
 )
 
 
@@ -73,6 +120,13 @@ def load(path: str | None = None):
         raise RaeError(f"{p} not found: build the HIP extension first "
                        "(python __graft_entry__.py build)")
     lib = C.CDLL(p)
+    lib.rae_build_id.restype = C.c_char_p
+    if path is None and "RAE_LIB" not in os.environ:     # RAE_LIB: explicit variant builds
+        want = source_build_id()
+        got = lib.rae_build_id().decode()
+        if want is not None and got != want:
+            raise RaeError(f"{p} was built from other sources (build id {got}, sources {want}): "
+                           "rebuild it (python __graft_entry__.py build)")
     lib.rae_last_error.restype = C.c_char_p
     lib.rae_version.restype = C.c_int
     lib.rae_exchange_record_floats.restype = C.c_int64
@@ -97,10 +151,11 @@ def load(path: str | None = None):
     lib.rae_neg_sample.argtypes = [_P, C.c_int64, _P, C.c_int64, _P, _P]
     lib.rae_neg_sample_philox.argtypes = [_P, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, _P, _P]
     lib.rae_time_next.argtypes = [_P, _P, _P]
+    lib.rae_stream_copy.argtypes = [_P, _P, C.c_int64, _P]
     lib.rae_event_create.argtypes = [C.POINTER(_P)]
     lib.rae_event_destroy.argtypes = [_P]
     lib.rae_event_elapsed_ms.argtypes = [_P, _P, C.POINTER(C.c_float)]
-    for fn in ("rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
+    for fn in ("rae_stream_copy", "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
                "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
                "rae_step_forward_at", "rae_step_update_at",

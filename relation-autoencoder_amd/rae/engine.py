@@ -119,6 +119,11 @@ class TrainEngine:
                    "rae_plan_create")
         self.plan = handle
         self.index_window = int(self.lib.rae_index_window(self.plan))
+        # a batch with more records than one LDS sort holds (RAE_KCAP / 2 = 4096, rae_common.hpp)
+        # is hash-partitioned, and a partition can overflow (a Zipf-heavy row at a large global
+        # batch): then run() checks the device error word after building each window's index,
+        # before any step of the window applies an update
+        self._index_partitioned = self.L * (2 + 2 * self.s) > 4096 or mbn > 4096
         self._graphs = {}
         self._epoch_mode = None
 
@@ -237,29 +242,63 @@ class TrainEngine:
         self._ensure_epoch_mode()
         self._graph(int(count or self.graph_chunk))
 
-    def run(self, first_batch: int, count: int, graph: bool = True):
-        """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
-        negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
-        of each window of batches is built right before the window's steps."""
-        self._ensure_epoch_mode()
-        b, end = int(first_batch), int(first_batch) + int(count)
+    def windows(self, first_batch: int, count: int):
+        """The index windows run() walks: [(first batch, batches), ...]."""
+        out, b, end = [], int(first_batch), int(first_batch) + int(count)
         while b < end:
             n = min(self.index_window, end - b)
+            out.append((b, n))
+            b += n
+        return out
+
+    def graph_sizes(self, first_batch: int, count: int):
+        """Step counts of the graphs run() replays for these batches: graph_chunk-step
+        graphs, plus one graph for each window's remainder (so no step runs eagerly)."""
+        if self.graph_chunk <= 1:
+            return []
+        sizes = []
+        for _, n in self.windows(first_batch, count):
+            full, rem = divmod(n, self.graph_chunk)
+            sizes += [self.graph_chunk] * full + ([rem] if rem else [])
+        return sizes
+
+    def capture_for(self, first_batch: int, count: int):
+        """Capture (without running) every graph run(first_batch, count) will replay, so no
+        capture lands inside a timed region."""
+        self._ensure_epoch_mode()
+        for n in sorted(set(self.graph_sizes(first_batch, count))):
+            self._graph(n)
+
+    def build_index(self, first_batch: int, count: int):
+        """Row index of batches [first_batch, first_batch+count) (one window at most)."""
+        _lib.check(self.lib.rae_build_index(self.plan, int(first_batch), int(count), self._stream()),
+                   "rae_build_index")
+
+    def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True):
+        """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
+        negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
+        of each window of batches is built right before the window's steps (index=False:
+        the caller built it already, e.g. bench.py ahead of its timed region).  With graph,
+        every step runs inside a replayed HIP graph: graph_chunk-step graphs and one graph
+        per window remainder."""
+        self._ensure_epoch_mode()
+        for b, n in self.windows(first_batch, count):
             st = self._stream()
-            _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
+            if index:
+                _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
+                if self._index_partitioned:
+                    self.check()
             _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
             if not graph or self.graph_chunk <= 1:
                 self._steps_eager(n, st)
             else:
-                T = self.graph_chunk
-                full, rem = divmod(n, T)
+                full, rem = divmod(n, self.graph_chunk)
                 if full:
-                    g = self._graph(T)
+                    g = self._graph(self.graph_chunk)
                     for _ in range(full):
                         g.replay()
                 if rem:
-                    self._steps_eager(rem, self._stream())
-            b += n
+                    self._graph(rem).replay()
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):

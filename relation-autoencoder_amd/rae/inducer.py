@@ -107,10 +107,18 @@ class ReconstructInducer:
         self.epoch_costs = []
         self.engine = None
         self.optimizer = None
+        self._resume = False        # set by load_checkpoint: keep optimizer state + epoch cursor
 
     def initialize(self):
-        """OieInduction.py:103-108: re-draw all parameters from the shared RNG."""
+        """OieInduction.py:103-108: re-draw all parameters from the shared RNG.  Like the
+        reference, the next train()/learn() then starts from epoch 0 with a fresh optimizer
+        (compile_function builds a new zero-accumulator AdaGrad, OieInduction.py:137)."""
         self._drop_engine()
+        self.optimizer = None
+        self._resume = False
+        self.cur_epoch = 0
+        self.train_errors = []
+        self.epoch_costs = []
         self.modelFunc = OieModelFunctions(self.rng, self.embedSize, self.relationNum,
                                            self.neg_sample_num, self.batch_size,
                                            self.decoder_type, self.data, self.extendedReg,
@@ -127,8 +135,10 @@ class ReconstructInducer:
     def compile_function(self):
         """OieInduction.py:118-155: build the train function and one labelling function
         per split."""
-        if self.optimizer is None:          # (kept when a checkpoint was loaded first)
-            self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)   # :137
+        if self.optimizer is None or not self._resume:
+            # a fresh zero-accumulator optimizer per compile, as the reference builds one
+            # (:137); only a loaded checkpoint keeps its accumulators
+            self.optimizer = make_optimizer(self.optimization, self.modelFunc.params)
         self.engine = TrainEngine(self.modelFunc, self.optimizer, self.data.split["train"],
                                   learning_rate=self.learningRate, lambda1=self.lambdaL1,
                                   lambda2=self.lambdaL2, world_size=self.world_size,
@@ -173,7 +183,10 @@ class ReconstructInducer:
         if not self._check_for_compiled_functions():
             self.compile_function()
         nb = self.batch_reps["train"]
-        epoch = self.cur_epoch                  # 0, or the epoch a checkpoint was taken at
+        # the reference always starts at epoch 0 (:175); a loaded checkpoint resumes at the
+        # epoch it was taken at
+        epoch = self.cur_epoch if self._resume else 0
+        self._resume = False
         while epoch < self.nb_epochs:
             t0 = time.perf_counter()
             epoch += 1
@@ -191,6 +204,11 @@ class ReconstructInducer:
                     if self._mode() == 1:
                         print(b * self.batch_size, b, "#" * 60)
                         print(self.get_clusters_size(), "\n")
+                    else:                       # mode 2: valid + test after every batch
+                        print(b * self.batch_size, b, "#" * 60)
+                        for split in SPLIT_LABELS[1:]:
+                            self.cluster[split] = self.get_clusters_sets(split)
+                            self._evaluate(split, verbose=verbose)
             else:
                 self.engine.run(0, nb)
             costs = self.engine.costs[:nb].double().cpu().numpy()
@@ -291,3 +309,4 @@ class ReconstructInducer:
                             float(z["rng_gauss"])))
         self.cur_epoch = int(z["epoch"])
         self.train_errors = [float(x) for x in z["train_errors"]]
+        self._resume = True

@@ -13,6 +13,7 @@ MODE
   gpu        the real HIP path with world_size 2: both ranks share cuda:0, the exchange
              records go through gloo (host-staged), eager steps.  Each rank saves its
              params and per-batch costs.
+  gpu_c3     the same at BASELINE config 3's full size with global batch L = 800 (2 x 400).
 """
 import os
 import sys
@@ -103,6 +104,32 @@ def run_gpu(out, decoder):
              costs=np.concatenate(ind.epoch_costs), **params)
 
 
+def run_gpu_c3(out, steps=3):
+    """BASELINE config 3 at full size (1M triples) with the global batch of 8 ranks at l=100,
+    L = 800, split over 2 ranks of l = 400: the first `steps` batches of an epoch, negatives
+    from the reference's RandomState stream (device CDF search)."""
+    from rae import dist as rdist
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    data, gold = synthetic_dataset(1_000_000, 2 ** 17, 100, seed=1234)
+    ex = rdist.make_exchange(ws, rk)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 800 // ws, 200, 100,
+                             20, 0.0, 0.0, "adagrad", "dp800", "sp", False, True, False, 1.0,
+                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1)
+    ind.compile_function()
+    eng = ind.engine
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    eng.run(0, steps)
+    torch.cuda.synchronize()
+    eng.check()
+    np.save(os.path.join(out, f"c3_costs_{rk}.npy"), eng.costs[:steps].cpu().numpy())
+    for k, v in ind.modelFunc.named_params().items():
+        np.save(os.path.join(out, f"c3_{k}_{rk}.npy"), v.detach().cpu().numpy())
+
+
 def main():
     mode, out = sys.argv[1], sys.argv[2]
     dec = sys.argv[3] if len(sys.argv) > 3 else "sp"
@@ -115,6 +142,8 @@ def main():
             run_oracle(out, dec, lambda1=float(sys.argv[4]) if len(sys.argv) > 4 else 0.0)
         elif mode == "gpu":
             run_gpu(out, dec)
+        elif mode == "gpu_c3":
+            run_gpu_c3(out)
         else:
             raise SystemExit(f"unknown mode {mode}")
         dist.barrier()

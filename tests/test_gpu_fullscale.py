@@ -13,6 +13,7 @@ size-independent property: every row the batches did not reference is bit-unchan
 """
 import numpy as np
 import pytest
+import scipy.sparse as sp
 
 import rae_oracle as O
 
@@ -50,6 +51,20 @@ def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234):
     return np.array(want), got, tr.params, params, init
 
 
+def _run_oracle_only(N, d, m, r, s, l, ntrue, steps, seed_data=1234):
+    from rae.data import synthetic_dataset
+    data, gold = synthetic_dataset(N, d, ntrue, seed=seed_data)
+    xs = data.split["train"]
+    tr = O.OracleTrainer("sp", xs.xFeats, xs.args1, xs.args2, data.negSamplingCum,
+                         np.random.RandomState(2), m, r, s, l, lr=0.1, alpha=1.0)
+    init = {k: v.copy() for k, v in tr.params.items()}
+    neg1 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+    neg2 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+    want = [tr.train_batch(b, neg1[:, O.batch_rows(b, l)], neg2[:, O.batch_rows(b, l)])
+            for b in range(steps)]
+    return np.array(want), None, tr.params, None, init
+
+
 def _check(want_c, got_c, want_p, got_p, init, min_untouched=0.0):
     np.testing.assert_allclose(got_c, want_c, rtol=COST_RTOL, atol=0)
     for k in want_p:
@@ -85,3 +100,123 @@ def test_c3_global_batch_800(built_lib, cuda_dev):
     want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=1_000_000, d=2 ** 17, m=100, r=200,
                                               s=20, l=800, ntrue=100, steps=3)
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
+
+
+# --------------------------------------------------------------------------------------------
+# config C4 at its real size: 10M synthetic triples, d = 2^20, K = 300, embed 300, neg 50, l=100
+# --------------------------------------------------------------------------------------------
+def _chunked_rows(draw, nrows, ncols, keep, chunk=1 << 16):
+    """Rows `keep` (sorted) of a (nrows, ncols) RandomState draw made in row chunks -- the same
+    stream as one whole draw (the legacy generator's doubles / cached Gaussians carry over
+    between calls) without materialising the whole matrix."""
+    out = np.empty((len(keep), ncols), dtype=np.float64)
+    for r0 in range(0, nrows, chunk):
+        blk = draw((min(chunk, nrows - r0), ncols))
+        lo, hi = np.searchsorted(keep, [r0, r0 + blk.shape[0]])
+        out[lo:hi] = blk[keep[lo:hi] - r0]
+    return out
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_size(built_lib, cuda_dev):
+    """BASELINE config 4 on one GPU at full size: the first steps of an epoch (graph-captured
+    epoch path, device negatives on the reference's RandomState stream) against the float64
+    oracle.  The oracle keeps only the rows the steps reference -- exact for lambda = 0,
+    because an AdaGrad step with zero gradient leaves a row bit-unchanged
+    (learning/Optimizers.py:30-32) -- drawn from the same RandomState(2) stream
+    in the reference's order (W, A, C1, C2; OieModel.py:49-63,105) without materialising the
+    2.5 GB W / 4.5 GB A in float64.  Checked: per-batch costs, every referenced row of W, A,
+    Ab and all of C1, C2, Wb; the initial values of the referenced rows; and a sample of
+    100k unreferenced rows of W and of A bit-unchanged over the steps."""
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    N, d, m, r, s, l, steps = 10_000_000, 2 ** 20, 300, 300, 50, 100, 3
+    data, gold = synthetic_dataset(N, d, 300, seed=1234)
+    xs = data.split["train"]
+    n = data.get_arg_voc_size()
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "c4", "sp", False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=2)
+    ind.compile_function()
+    eng = ind.engine
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")   # neg1 then neg2, (s, N) each
+    rows = slice(0, steps * l)
+    neg1 = eng.neg1[:, rows].cpu().numpy()
+    neg2 = eng.neg2[:, rows].cpu().numpy()
+    Xb = xs.xFeats[rows]
+    tf = np.unique(Xb.indices)
+    te = np.unique(np.concatenate([xs.args1[rows], xs.args2[rows], neg1.ravel(), neg2.ravel()]))
+    named = ind.modelFunc.named_params()
+    g = np.random.RandomState(99)
+    uf = np.setdiff1d(g.choice(d, 100_000, replace=False), tf)
+    ue = np.setdiff1d(g.choice(n, 100_000, replace=False), te)
+    uf_t, ue_t = torch.as_tensor(uf, device=cuda_dev), torch.as_tensor(ue, device=cuda_dev)
+    W0 = named["W"][uf_t].cpu().numpy()
+    A0 = named["A"][ue_t].cpu().numpy()
+    init_W = named["W"][torch.as_tensor(tf, device=cuda_dev)].cpu().double().numpy()
+    init_A = named["A"][torch.as_tensor(te, device=cuda_dev)].cpu().double().numpy()
+
+    eng.run(0, steps)
+    torch.cuda.synchronize()
+    eng.check()
+    got_c = eng.costs[:steps].cpu().numpy().astype(np.float64)
+
+    # the oracle on the referenced rows, same RandomState(2) draws
+    rng = np.random.RandomState(2)
+    p = {"W": _chunked_rows(lambda sh: rng.uniform(O.LOW, O.HIGH, sh), d, m, tf),
+         "Wb": np.zeros(m)}
+    p["A"] = _chunked_rows(lambda sh: rng.uniform(-0.01, 0.01, sh), n, r, te)
+    p["C1"] = rng.normal(0, np.sqrt(0.1), (r, m))
+    p["C2"] = rng.normal(0, np.sqrt(0.1), (r, m))
+    p["Ab"] = np.zeros(len(te))
+    assert np.array_equal(init_W, p["W"].astype(np.float32).astype(np.float64))
+    assert np.array_equal(init_A, p["A"].astype(np.float32).astype(np.float64))
+    assert np.array_equal(named["C1"].cpu().double().numpy(),
+                          p["C1"].astype(np.float32).astype(np.float64))
+    acc = {k: np.zeros_like(v) for k, v in p.items()}
+    fmap = np.full(d, -1, np.int64)
+    fmap[tf] = np.arange(len(tf))
+    emap = np.full(n, -1, np.int64)
+    emap[te] = np.arange(len(te))
+    want_c = []
+    for b in range(steps):
+        rb = slice(b * l, (b + 1) * l)
+        Xs = xs.xFeats[rb]
+        Xc = sp.csr_matrix((Xs.data, fmap[Xs.indices], Xs.indptr), shape=(l, len(tf)))
+        res = O.train_step_grads("sp", p, Xc, emap[xs.args1[rb]], emap[xs.args2[rb]],
+                                 emap[neg1[:, rb]], emap[neg2[:, rb]], alpha=1.0)
+        O.adagrad_apply(p, acc, res.grads, 0.1)
+        want_c.append(res.cost)
+    np.testing.assert_allclose(got_c, np.array(want_c), rtol=COST_RTOL, atol=0)
+    got = {"W": named["W"][torch.as_tensor(tf, device=cuda_dev)],
+           "A": named["A"][torch.as_tensor(te, device=cuda_dev)],
+           "Ab": named["Ab"][torch.as_tensor(te, device=cuda_dev)],
+           "C1": named["C1"], "C2": named["C2"], "Wb": named["Wb"]}
+    for k, v in got.items():
+        v = v.cpu().double().numpy()
+        err = np.abs(v - p[k])
+        tol = 2e-4 + 2e-3 * np.abs(p[k])
+        assert np.all(err <= tol), f"{k}: max err {err.max():.3e}"
+    assert np.array_equal(named["W"][uf_t].cpu().numpy(), W0)
+    assert np.array_equal(named["A"][ue_t].cpu().numpy(), A0)
+
+
+def test_c3_global_batch_800_two_ranks(built_lib, cuda_dev, tmp_path):
+    """The data-parallel path itself at C3's full size: 2 ranks x l = 400 (the global batch of
+    8 ranks at l = 100), records all-gathered between the forward and the update, against the
+    float64 oracle at the global batch L = 800; the two replicas bit-identical."""
+    import test_dist
+    test_dist._launch(["gpu_c3", str(tmp_path)], timeout=600)
+    want_c, _, want_p, _, init = _run_oracle_only(N=1_000_000, d=2 ** 17, m=100, r=200, s=20,
+                                                  l=800, ntrue=100, steps=3)
+    c0 = np.load(tmp_path / "c3_costs_0.npy").astype(np.float64)
+    c1 = np.load(tmp_path / "c3_costs_1.npy").astype(np.float64)
+    np.testing.assert_array_equal(c0, c1)
+    got = {}
+    for k in want_p:
+        g0 = np.load(tmp_path / f"c3_{k}_0.npy")
+        g1 = np.load(tmp_path / f"c3_{k}_1.npy")
+        assert np.array_equal(g0, g1), f"replicas differ in {k}"
+        got[k] = g0.astype(np.float64)
+    _check(want_c, c0, want_p, got, init, min_untouched=0.5)

@@ -499,3 +499,101 @@ def test_hot_rows_vs_oracle(built_lib, cuda_dev, dec):
     tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
     np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
     _assert_params_close(_params(ind), tr.params, "hot")
+
+
+def test_initialize_then_train_restarts_like_reference(built_lib, cuda_dev):
+    """test.py:33-46's sequence: train(), initialize(), train().  The second train() runs all
+    its epochs again from epoch 0 with a fresh zero-accumulator optimizer
+    (OieInduction.py:103-108,137,175) on parameters re-drawn from the same shared RNG."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l, ep = 8, 16, 4, 50, 2
+    data, gold = synthetic_dataset(400, 300, 4, seed=9)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), ep, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "restart", "sp", False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2)
+    ind.train()
+    first = np.array(ind.epoch_costs)
+    ind.initialize()
+    assert ind.cur_epoch == 0 and ind.optimizer is None
+    ind.train()
+    assert ind.cur_epoch == ep
+    second = np.array(ind.epoch_costs)
+    assert second.shape == first.shape
+    # the oracle: one RandomState drives init, epoch negatives, re-init, epoch negatives
+    xs = data.split["train"]
+    rng = np.random.RandomState(2)
+    tr = O.OracleTrainer("sp", xs.xFeats, xs.args1, xs.args2, data.negSamplingCum, rng, m, r, s,
+                         l, lr=0.1, alpha=1.0)
+    want1 = np.array([tr.epoch()[0] for _ in range(ep)])
+    tr2 = O.OracleTrainer("sp", xs.xFeats, xs.args1, xs.args2, data.negSamplingCum, rng, m, r, s,
+                          l, lr=0.1, alpha=1.0)          # re-draw + zero accumulators
+    want2 = np.array([tr2.epoch()[0] for _ in range(ep)])
+    np.testing.assert_allclose(first, want1, rtol=COST_RTOL, atol=COST_RTOL)
+    np.testing.assert_allclose(second, want2, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr2.params, "restart")
+
+
+def test_frequent_eval_mode2_evaluates_valid_and_test_every_batch(built_lib, cuda_dev, capsys):
+    """frequentEval with train/valid/test splits (mode 2): after every batch the valid and
+    test clusters are labelled and B^3-evaluated (OieInduction.py:194-198), and again at the
+    end of every epoch (:214-217)."""
+    from rae.data import DatasetManager, DatasetSplit, synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    full, gold = synthetic_dataset(300, 200, 3, seed=4)
+    xs = full.split["train"]
+    cut = [slice(0, 200), slice(200, 250), slice(250, 300)]
+    splits = {k: DatasetSplit(xs.args1[c], xs.args2[c], xs.xFeats[c])
+              for k, c in zip(("train", "valid", "test"), cut)}
+    g = {k: {i - c.start: v for i, v in gold["train"].items() if c.start <= i < c.stop}
+         for k, c in zip(("train", "valid", "test"), cut)}
+    for k in ("valid", "test"):
+        g[k].setdefault(0, ["REL0"])            # at least one gold label per split
+    data = DatasetManager(splits, full.entity_freqs, full.n_features)
+    ind = ReconstructInducer(data, g, np.random.RandomState(2), 2, 0.1, 25, 8, 4, 3, 0.0, 0.0,
+                             "adagrad", "mode2", "sp", False, True, True, 1.0, device=cuda_dev)
+    ind.learn()
+    out = capsys.readouterr().out
+    nb = 200 // 25
+    assert out.count("valid f1:") == 2 * (nb + 1)
+    assert out.count("test f1:") == 2 * (nb + 1)
+
+
+def test_label_argmax_nan_and_inf_follow_numpy(built_lib, cuda_dev):
+    """A diverged row still gets a label in [0, m): argmax treats NaN as the maximum (first
+    NaN wins) and an all -inf row gives 0, as numpy's / Theano's argmax do."""
+    import torch
+    from rae.engine import DeviceSplit
+    from rae.data import DatasetSplit
+    from rae import _lib
+    import ctypes as C
+    g = np.random.RandomState(1)
+    N, d, m = 64, 30, 12
+    rows = np.repeat(np.arange(N), 3)
+    X = sp.csr_matrix((np.ones(3 * N, np.float32), (rows, g.randint(0, d, 3 * N))), shape=(N, d))
+    X.sum_duplicates()
+    X.data[:] = 1.0
+    W = g.uniform(-1, 1, (d, m)).astype(np.float32)
+    Wb = np.zeros(m, np.float32)
+    W[5, 7] = np.nan
+    W[5, 3] = np.nan
+    W[9, :] = -np.inf
+    ds = DeviceSplit(DatasetSplit(np.zeros(N), np.zeros(N), X), cuda_dev)
+    Wt = torch.as_tensor(W, device=cuda_dev)
+    Wbt = torch.as_tensor(Wb, device=cuda_dev)
+    lab = torch.empty(N, dtype=torch.int64, device=cuda_dev)
+    lib = _lib.load()
+    _lib.check(lib.rae_label(C.c_void_p(ds.indptr.data_ptr()), C.c_void_p(ds.indices.data_ptr()),
+                             None, C.c_void_p(Wt.data_ptr()), C.c_void_p(Wbt.data_ptr()), m, 0, N,
+                             C.c_void_p(lab.data_ptr()), None, None), "rae_label")
+    torch.cuda.synchronize()
+    Xd = X.toarray().astype(np.float64)
+    S = np.zeros((N, m))
+    for i in range(N):                       # S = X.W + Wb with inf/nan propagation per row
+        S[i] = sum(Xd[i, f] * W[f].astype(np.float64) for f in np.nonzero(Xd[i])[0]) + Wb
+    want = np.argmax(S, axis=1)
+    got = lab.cpu().numpy()
+    assert np.all((got >= 0) & (got < m))
+    special = ~np.all(np.isfinite(S), axis=1)
+    assert special.sum() > 0
+    assert np.array_equal(got[special], want[special])
