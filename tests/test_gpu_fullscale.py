@@ -156,6 +156,7 @@ def test_c4_full_size(built_lib, cuda_dev):
     A0 = named["A"][ue_t].cpu().numpy()
     init_W = named["W"][torch.as_tensor(tf, device=cuda_dev)].cpu().double().numpy()
     init_A = named["A"][torch.as_tensor(te, device=cuda_dev)].cpu().double().numpy()
+    init_C1 = named["C1"].cpu().double().numpy()
 
     eng.run(0, steps)
     torch.cuda.synchronize()
@@ -172,8 +173,7 @@ def test_c4_full_size(built_lib, cuda_dev):
     p["Ab"] = np.zeros(len(te))
     assert np.array_equal(init_W, p["W"].astype(np.float32).astype(np.float64))
     assert np.array_equal(init_A, p["A"].astype(np.float32).astype(np.float64))
-    assert np.array_equal(named["C1"].cpu().double().numpy(),
-                          p["C1"].astype(np.float32).astype(np.float64))
+    assert np.array_equal(init_C1, p["C1"].astype(np.float32).astype(np.float64))
     acc = {k: np.zeros_like(v) for k, v in p.items()}
     fmap = np.full(d, -1, np.int64)
     fmap[tf] = np.arange(len(tf))
