@@ -122,81 +122,134 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 #define RAE_WAVE_END() do { } while (0)
 #endif
 
+// Update launch layout (workgroups of RAE_NWAVE = 4 waves), in dispatch order:
+//   [0, nT)              one dense 16x16 tile per workgroup: C1/C2 tiles, then Wb tiles
+//                        (no row index needed: they start at once; K = batch split 4 ways)
+//   [nT, nT + nP)        one wave task each, no row index needed: the cost, R-row blocks
+//   then, after the batch's index header: one workgroup per very heavy A row, per very heavy
+//   W row, and the remaining workgroups' waves grid-stride over the heavy A rows, heavy W
+//   rows, light A rows, light W rows (one row per wave)
+__host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
+    return 1 + n_rtiles(dec, r, m);                      // the cost + R/C row blocks
+}
+#ifndef RAE_UPD_WGCAP
+#define RAE_UPD_WGCAP 1536    // row-task workgroups: 6 per CU (24 waves) on 256 CUs
+#endif
+__host__ __device__ inline int64_t update_grid(int dec, int r, int m, int RA, int RW, int VCA, int VCW) {
+    const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
+    const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
+    int64_t rows = ((int64_t)RA + RW + RAE_NWAVE - 1) / RAE_NWAVE;
+    if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
+    return (int64_t)nT + nP + VCA + VCW + rows;
+}
+
 template <int OPT, bool V4, int Q, bool BIL>
 __device__ __forceinline__ void update_body(const StepArgs& a) {
+    typedef typename VecT<V4>::T VT;
+    // workgroup tasks' partials: a row (Q vectors per lane) or a tile (4 floats per lane) per wave
+    constexpr int kRowF = RAE_NWAVE * Q * RAE_WAVE * (V4 ? 4 : 1), kTileF = RAE_NWAVE * RAE_WAVE * 4;
+    __shared__ __attribute__((aligned(16))) float spart_f[kRowF > kTileF ? kRowF : kTileF];
+    __shared__ float sgb[RAE_NWAVE];
+    VT* spart = reinterpret_cast<VT*>(spart_f);
     const int lane = threadIdx.x & 63;
-    // the wave index as a provably uniform value: every task index, row id and record
-    // offset derived from it is then scalar (s_load of the segment, SGPR soffsets, scalar
-    // branches) instead of VGPR-resident and exec-masked
-    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
-    const int nw = gridDim.x * RAE_NWAVE;
+    // wave / workgroup indices as provably uniform values: every task index, row id and
+    // record offset derived from them is then scalar (s_load of the segment, SGPR soffsets,
+    // scalar branches) instead of VGPR-resident and exec-masked
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    const int gw = wg * RAE_NWAVE + w;
     const int64_t g = step_batch(a);
     const int64_t ex0 = g * (int64_t)a.L;
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
     const int nCt = n_ctiles(a.dec, a.r, a.m);
     const int nRt = n_rtiles(a.dec, a.r, a.m);
+    const int nT = nCt + mt;
+    const int nPt = update_wave_free_tasks(a.dec, a.r, a.m);
+    const int nP = (nPt + RAE_NWAVE - 1) / RAE_NWAVE;
     const int64_t slot = g % a.index_window;
-    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];   // records, rows, heavy rows
-    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
-    const int TA = hA.y, HA = hA.z, TW = hW.y, HW = hW.z;
-    // Task order = dispatch order: the heavy rows (Zipf-frequent entities / features, the
-    // longest tasks) first, then the dense tiles and the cost, then the light rows.
-    const int nD = nCt + nRt + mt + 1;
-    const int T = TA + TW + nD;
 #ifdef RAE_STAMPS
     unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    int first_type = -1;
+#define RAE_FIRST(kind_)                                                                    \
+    do {                                                                                    \
+        if (a.stamps && lane == 0) {                                                        \
+            a.stamps[(size_t)gw * 4 + 0] = t_start;                                         \
+            a.stamps[(size_t)gw * 4 + 1] = (unsigned long long)(kind_);                     \
+        }                                                                                   \
+    } while (0)
+#else
+#define RAE_FIRST(kind_) do { } while (0)
 #endif
-    for (int t = gw; t < T; t += nw) {
-        // task -> (kind, index): kind 0 C-tile, 1 R-tile, 2 Wb-tile, 3 cost, 4 A row, 5 W row;
-        // for rows, x = the segment slot (heavy x = u, light x = cap-1-v; rae_index.hpp)
-        int kind, x;
-        if (t < HA) { kind = 4; x = t; }
-        else if (t < HA + HW) { kind = 5; x = t - HA; }
-        else if (t < HA + HW + nD) {
-            x = t - HA - HW;
-            if (x < nCt) kind = 0;
-            else if ((x -= nCt) < nRt) kind = 1;
-            else if ((x -= nRt) < mt) kind = 2;
-            else { kind = 3; x = 0; }
+    if (wg < nT) {                                            // dense tiles
+#ifndef RAE_SKIP_TILES
+        RAE_FIRST(wg < nCt ? 0 : 2);
+        if (wg < nCt) {
+            const int which = wg / (rt * mt), ti = wg - which * rt * mt;
+            wg_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
+                         which ? a.lay.odw2 : a.lay.odw1, false, (ti / mt) * 16, (ti % mt) * 16,
+                         wg, w, lane, reinterpret_cast<rae_f4*>(spart));
         } else {
-            const int v = t - HA - HW - nD;
-            if (v < TA - HA) { kind = 4; x = a.RA - 1 - v; }
-            else { kind = 5; x = a.RW - 1 - (v - (TA - HA)); }
-        }
-#ifdef RAE_STAMPS
-        if (first_type < 0) {
-            first_type = (kind >= 4 && t < HA + HW) ? kind + 2 : kind;   // 6/7: heavy rows
-            if (a.stamps && lane == 0) {
-                a.stamps[(size_t)gw * 4 + 0] = t_start;
-                a.stamps[(size_t)gw * 4 + 1] = (unsigned long long)first_type;
-            }
-        }
-#endif
-#ifdef RAE_SKIP_TILES
-        if (kind < 4) continue;     // diagnostic: row tasks alone
-#endif
-#ifdef RAE_SKIP_ROWS
-        if (kind >= 4) continue;    // diagnostic: tile tasks alone
-#endif
-        if (kind == 0) {
-            const int which = x / (rt * mt), ti = x - which * rt * mt;
-            task_mfma_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
-                                which ? a.lay.odw2 : a.lay.odw1, false, (ti / mt) * 16,
-                                (ti % mt) * 16, x, lane);
-        } else if (BIL && kind == 1) {
-            task_bilinear_rows<OPT>(a, x, nCt + x, lane);
-        } else if (kind == 2) {
-            task_mfma_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, x * 16, 0, lane);
-        } else if (kind == 3) {
-            task_cost(a, lane);
-        } else if (kind == 4) {
-            task_entity_row<OPT, V4, Q, BIL>(a, slot, x, lane);
-        } else {
-            task_feature_row<OPT, V4, Q>(a, ex0, slot, x, lane);
+            wg_tile<OPT>(a, a.Wb, a.aWb, 1, 0, true, 0, (wg - nCt) * 16, 0, w, lane,
+                         reinterpret_cast<rae_f4*>(spart));
         }
         RAE_WAVE_END();
+#endif
+        return;
     }
+    if (wg < nT + nP) {                                       // cost, R-row blocks
+        const int t = (wg - nT) * RAE_NWAVE + w;
+#ifndef RAE_SKIP_TILES
+        if (t == 0) {
+            RAE_FIRST(3);
+            task_cost(a, lane);
+        } else if (t < nPt) {
+            RAE_FIRST(1);
+            if constexpr (BIL) task_bilinear_rows<OPT>(a, t - 1, nCt + t - 1, lane);
+        }
+        RAE_WAVE_END();
+#endif
+        return;
+    }
+    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];   // records, rows, heavy, very heavy
+    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
+    const int HA = hA.z, HW = hW.z, LA = hA.y - hA.z, LW = hW.y - hW.z, VA = hA.w, VW = hW.w;
+    const int u = wg - nT - nP;
+#ifdef RAE_SKIP_ROWS
+    return;                                                   // diagnostic: dense tasks alone
+#endif
+    if (u < VA + VW) {                                        // very heavy rows
+        RAE_FIRST(u < VA ? 8 : 9);
+        if (u < VA) wg_entity_row<OPT, V4, Q, BIL>(a, slot, u, w, lane, spart, sgb);
+        else wg_feature_row<OPT, V4, Q>(a, ex0, slot, u - VA, w, lane, spart);
+        RAE_WAVE_END();
+        return;
+    }
+    // row tasks: heavy A, heavy W, light A, light W; a wave with several tasks (large global
+    // batches: the grid's row part is capped near one resident wave per slot) loads its next
+    // task's segment while it works on the current one
+    const int nw = (gridDim.x - nT - nP - VA - VW) * RAE_NWAVE;
+    const int T = HA + HW + LA + LW;
+    auto seg_of = [&](int t, bool& isA) {
+        int x = t;
+        if (x < HA) { isA = true; }
+        else if ((x -= HA) < HW) { isA = false; }
+        else if ((x -= HW) < LA) { isA = true; x = a.RA - 1 - x; }
+        else { isA = false; x = a.RW - 1 - (x - LA); }
+        return row_segment(a, slot, isA, x);
+    };
+    int t = (u - VA - VW) * RAE_NWAVE + w;
+    bool isA = true, nA = true;
+    int4 seg = t < T ? seg_of(t, isA) : make_int4(0, 0, 0, 0);
+    for (; t < T; t += nw) {
+        const int4 cur = seg;
+        const bool curA = isA;
+        if (t + nw < T) seg = seg_of(t + nw, nA);
+        RAE_FIRST(curA ? (t < HA ? 6 : 4) : (t < HA + HW ? 7 : 5));
+        if (curA) task_entity_row<OPT, V4, Q, BIL>(a, slot, cur, lane);
+        else task_feature_row<OPT, V4, Q>(a, ex0, slot, cur, lane);
+        isA = nA;
+        RAE_WAVE_END();
+    }
+#undef RAE_FIRST
 }
 
 // SP and bilinear variants (the bilinear R-row tasks need more registers).
@@ -488,6 +541,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_hdrA = take(16 * W_), o_hdrW = take(16 * W_);
     const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(16ull * W_ * a.RA);
     const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(16ull * W_ * a.RW);
+    a.VCA = a.RA / (RAE_VHEAVY + 1) + 1;       // very heavy rows per batch are fewer than this
+    a.VCW = a.RW / (RAE_VHEAVY + 1) + 1;
+    const size_t o_vrowA = take(16ull * W_ * a.VCA), o_vrowW = take(16ull * W_ * a.VCW);
     {
         const int NJd = 2 + 2 * c.neg_samples;
         int cap = c.max_row_nnz > 0 ? c.max_row_nnz : 1;
@@ -531,6 +587,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
+    a.vrowA = reinterpret_cast<int32_t*>(p->ws + o_vrowA);
+    a.vrowW = reinterpret_cast<int32_t*>(p->ws + o_vrowW);
 
     a.desc = reinterpret_cast<int32_t*>(p->ws + o_desc);
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
@@ -553,9 +611,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
     }
     p->grid_fwd = c.batch_size;
-    const int64_t tasks = (int64_t)a.RA + a.RW + a.nregC + (c.relations + 15) / 16 + 1;  // upper bound
-    int gu = ceil_div(tasks, RAE_NWAVE);
-    p->grid_update = gu < 1 ? 1 : (gu > 8192 ? 8192 : gu);
+    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.RA, a.RW, a.VCA, a.VCW);
+    if (gu >= (1ll << 31)) {
+        (void)hipFree(p->ws);
+        delete p;
+        return fail(RAE_E_INVALID, "update grid too large");
+    }
+    p->grid_update = (int)gu;
     {
         const void* fns[] = {(const void*)k_forward<true, DimsC3>,
                              (const void*)k_forward<false, DimsC2>,

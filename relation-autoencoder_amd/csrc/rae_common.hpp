@@ -12,6 +12,9 @@
 #define RAE_KCAP 8192         // LDS capacity (64-bit keys) of one row-index partition
 #define RAE_PART 256          // target records per row-index partition
 #define RAE_HEAVY 4           // a parameter row with more records than this per step is "heavy"
+#ifndef RAE_VHEAVY
+#define RAE_VHEAVY 16         // ... than this: "very heavy", split over a workgroup's four waves
+#endif
 
 namespace rae {
 

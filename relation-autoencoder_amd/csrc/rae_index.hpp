@@ -14,14 +14,18 @@
 // parameters -- so it is built ahead of the steps, for a window of batches per launch
 // (k_build_index, one workgroup per (batch, A|W)), off the step's critical path.
 // Layout per batch slot (slot = batch % window):
-//   hdr[slot]            = (records, unique rows, heavy rows, 0)
+//   hdr[slot]            = (records, heavy + light rows, heavy rows, very heavy rows)
 //   srec[slot][i]        = record id, i in sorted order
 //   seg[slot][x]         = (row, first sorted position, end position, first record id) of a
-//                          unique row; rows with more than RAE_HEAVY records ("heavy": the
-//                          Zipf-frequent entities / features) fill x = 0, 1, ... and the light
-//                          rows fill x = Rcap-1, Rcap-2, ... so the update can hand the heavy
-//                          rows -- its longest tasks -- to the first-dispatched waves, and a
-//                          one-record row needs no srec read (its record rides in the segment)
+//                          unique row with at most RAE_VHEAVY records; rows with more than
+//                          RAE_HEAVY ("heavy": the Zipf-frequent entities / features) fill
+//                          x = 0, 1, ... and the light rows fill x = Rcap-1, Rcap-2, ... so the
+//                          update can hand the heavy rows -- its longest one-wave tasks -- to
+//                          the first-dispatched waves, and a one-record row needs no srec read
+//                          (its record rides in the segment)
+//   vseg[slot][x]        = the same for rows with more than RAE_VHEAVY records ("very heavy":
+//                          tens to hundreds of records at a large global batch), which the
+//                          update splits over the four waves of a workgroup
 // Records: A-index rec = b*NJ + j (j = 0 e1, 1 e2, 2+t neg1[t], 2+s+t neg2[t]);
 //          W-index rec = b << posbits | position of the feature in row b.
 // Rows are hash-partitioned (row % H) when a batch has more records than one LDS sort
@@ -91,6 +95,8 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     int32_t* hdr = (isA ? a.hdrA : a.hdrW) + 4 * slot;
     int32_t* srec = (isA ? a.srecA : a.srecW) + slot * (int64_t)Rcap;
     int4* seg = reinterpret_cast<int4*>(isA ? a.urowA : a.urowW) + slot * (int64_t)Rcap;
+    const int Vcap = isA ? a.VCA : a.VCW;
+    int4* vseg = reinterpret_cast<int4*>(isA ? a.vrowA : a.vrowW) + slot * (int64_t)Vcap;
     if (!isA)
         for (int b = tid; b <= a.L; b += BT) sptr[b] = a.indptr[ex0 + b];
     __syncthreads();
@@ -99,12 +105,12 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     if (nrec > Rcap) {
         if (tid == 0) {
             atomicOr(a.err, 4);
-            hdr[0] = hdr[1] = hdr[2] = 0;
+            hdr[0] = hdr[1] = hdr[2] = hdr[3] = 0;
         }
         return;
     }
     const int H = index_partitions(nrec);
-    int base_i = 0, nh = 0, nl = 0;
+    int base_i = 0, nh = 0, nl = 0, nv = 0;
     for (int h = 0; h < H; ++h) {
         if (tid == 0) sint[0] = 0;
         __syncthreads();
@@ -139,7 +145,7 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
         if (cnt > RAE_KCAP) {
             if (tid == 0) {
                 atomicOr(a.err, isA ? 1 : 2);
-                hdr[0] = hdr[1] = hdr[2] = 0;
+                hdr[0] = hdr[1] = hdr[2] = hdr[3] = 0;
             }
             return;
         }
@@ -165,7 +171,8 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
             nu += tot;
         }
         __syncthreads();
-        // segments -> heavy rows at the front, light rows at the back (order kept in each)
+        // segments -> very heavy rows to vseg, heavy rows at the front of seg, light rows at
+        // its back (order kept in each class)
         for (int v0 = 0; v0 < nu; v0 += BT) {
             const int v = v0 + tid;
             const bool valid = v < nu;
@@ -174,18 +181,22 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
                 st = sstart[v];
                 en = (v + 1 < nu) ? sstart[v + 1] : cnt;
             }
-            const bool heavy = valid && (en - st) > RAE_HEAVY;
-            int htot, ltot;
+            const bool vheavy = valid && (en - st) > RAE_VHEAVY;
+            const bool heavy = valid && !vheavy && (en - st) > RAE_HEAVY;
+            int htot, ltot, vtot;
             const int hp = block_flag_scan<BT>(heavy, sint + 1, &htot);
-            const int lp = block_flag_scan<BT>(valid && !heavy, sint + 12, &ltot);
+            const int lp = block_flag_scan<BT>(valid && (en - st) <= RAE_HEAVY, sint + 12, &ltot);
+            const int vp = block_flag_scan<BT>(vheavy, sint + 21, &vtot);
             if (valid) {
                 const unsigned long long k = keys[st];
-                const int x = heavy ? nh + hp : Rcap - 1 - (nl + lp);
-                seg[x] = make_int4((int)(unsigned)(k >> 32), base_i + st, base_i + en,
-                                   (int)(unsigned)(k & 0xffffffffull));
+                const int4 sg = make_int4((int)(unsigned)(k >> 32), base_i + st, base_i + en,
+                                          (int)(unsigned)(k & 0xffffffffull));
+                if (vheavy) vseg[nv + vp] = sg;
+                else seg[heavy ? nh + hp : Rcap - 1 - (nl + lp)] = sg;
             }
             nh += htot;
             nl += ltot;
+            nv += vtot;
         }
         base_i += cnt;
         __syncthreads();
@@ -194,7 +205,7 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
         hdr[0] = base_i;
         hdr[1] = nh + nl;
         hdr[2] = nh;
-        hdr[3] = 0;
+        hdr[3] = nv;
     }
 }
 

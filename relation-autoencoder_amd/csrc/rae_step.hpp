@@ -80,6 +80,8 @@ struct StepArgs {
     int64_t index_window;
     int32_t *hdrA, *srecA, *urowA;      // urow*: interleaved (row, first position) pairs
     int32_t *hdrW, *srecW, *urowW;
+    int32_t *vrowA, *vrowW;             // very heavy rows' segments (VCA / VCW per slot)
+    int VCA, VCW;
     // per-example descriptors of this rank's l examples per slot (rae_index.hpp):
     // [nf, p0, entity ids (NJ), feature ids (<= dcap)], dstride ints each
     int32_t* desc;

@@ -9,9 +9,11 @@
 // regulariser gradient: then the W rows are only reduced into a dense scratch here and the
 // dense sweep kernel (k_dense_w) applies the full update, as the reference does.
 //
-// Work items of k_update, one wavefront each (grid-strided):
-//   dense decoder-matrix tiles (16x16, MFMA), Wb tiles, the batch cost,
-//   one wave per referenced A row, one wave per referenced W row.
+// Work items of k_update:
+//   one workgroup (four waves, the batch split four ways) per dense decoder-matrix tile
+//   (16x16, MFMA) and Wb tile, and per very heavy A / W row (> RAE_VHEAVY records);
+//   one wavefront for the batch cost, for each bilinear R-row block, and for every other
+//   referenced A row and W row.
 #pragma once
 #include "rae_common.hpp"
 #include "rae_index.hpp"
@@ -40,58 +42,53 @@ typedef float rae_f4 __attribute__((ext_vector_type(4)));
 #endif
 template <int N> struct IntC { static constexpr int value = N; };
 
+// parameters + accumulators of the tile elements this lane updates (lanes >= 16 of a Wb tile
+// own nothing): loaded up front, in flight with the records
 template <int OPT>
-__device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw,
-                               bool ones, int i0, int k0, int slot, int lane) {
+__device__ __forceinline__ void tile_params(const StepArgs& a, const float* M, const float* aM,
+                                            int nrows, bool ones, int i0, int k0, int lane,
+                                            float pw[4], float pa[4]) {
+    const int li = lane & 15, lk = lane >> 4, col = k0 + li;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = i0 + lk * 4 + reg;
+        const bool ok = row < nrows && col < a.m && (!ones || row == i0);
+        const int o = ok ? (ones ? col : row * a.m + col) : 0;
+        pw[reg] = M[o];
+        pa[reg] = (OPT == 0) ? aM[o] : 0.f;
+    }
+}
+
+// the tile's MFMA chain over examples [b0, b1) of the global batch (b0 a multiple of 4)
+__device__ __forceinline__ rae_f4 tile_accum(const StepArgs& a, int nrows, int odw, bool ones,
+                                             int i0, int k0, int b0, int b1, int lane) {
     const int li = lane & 15, lk = lane >> 4;
     const int m = a.m, L = a.L;
     const int i = i0 + li, k = k0 + li;
     const bool iv = i < nrows, kv = k < m;
     const int ic = iv ? i : 0, kc = kv ? k : 0;
     rae_f4 acc = {0.f, 0.f, 0.f, 0.f};
-#ifdef RAE_ICACHE_TEST
-#pragma clang loop unroll(disable)
-    for (int rep = 0; rep < 2; ++rep) {
-    if (rep == 1) {
-        if (a.stamps && lane == 0) {
-            const int gw = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
-            if (slot == gw) a.stamps[(size_t)gw * 4 + 3] = __builtin_amdgcn_s_memrealtime();
-        }
-        acc = rae_f4{0.f, 0.f, 0.f, 0.f};
-    }
-#endif
     const int ox = odw + ic, oy = (ones ? a.lay.odS : a.lay.oP) + kc;   // Wb: sum_b dS_b
-    // the tile's parameters and accumulators are loaded up front, in flight with the records
-    const int col = k0 + li;
-    float pw[4], pa[4];
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        const int row = i0 + lk * 4 + reg;
-        const bool ok = row < nrows && col < m && (!ones || row == i0);
-        const int o = ok ? (ones ? col : row * m + col) : 0;
-        pw[reg] = M[o];
-        pa[reg] = (OPT == 0) ? aM[o] : 0.f;
-    }
     // L % 4 == 0 (every k-step's 4 examples exist): the k-step's first record offset is
     // wave-uniform and rides in the buffer load's soffset, the lane's (example, column) in
     // one voffset VGPR for all TU loads
     const RecBuf rb_(a.ex);
     const bool whole = (L & 3) == 0;
     const int rec = a.lay.rec, vx = lk * rec + ox, vy = lk * rec + oy;
-    for (int b0 = 0; b0 < L; b0 += 4 * RAE_TU) {
+    for (int bb = b0; bb < b1; bb += 4 * RAE_TU) {
         float av[RAE_TU], bv[RAE_TU];
         // every operand load goes out before the first MFMA: the sched_barrier keeps the
         // scheduler from sinking each load next to its MFMA (which serialised 32 round trips)
 #pragma unroll
         for (int u = 0; u < RAE_TU; ++u) {
-            const int bs = b0 + 4 * u;
+            const int bs = bb + 4 * u;
             if (whole) {
-                const int so = (bs < L ? bs : 0) * rec;
+                const int so = (bs < b1 ? bs : 0) * rec;
                 if (ones) av[u] = 1.f; else rb_.load(av[u], vx, so);
                 rb_.load(bv[u], vy, so);
             } else {
                 const int b = bs + lk;
-                const int rb = (b < L ? b : 0) * rec;
+                const int rb = (b < b1 ? b : 0) * rec;
                 av[u] = ones ? 1.f : a.ex[rb + ox];
                 bv[u] = a.ex[rb + oy];
             }
@@ -99,15 +96,20 @@ __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < RAE_TU; ++u) {
-            const bool bvld = b0 + 4 * u + lk < L;
+            const bool bvld = bb + 4 * u + lk < b1;
             const float x = (bvld && iv && (!ones || li == 0)) ? av[u] : 0.f;
             const float y = (bvld && kv) ? bv[u] : 0.f;
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, acc, 0, 0, 0);
         }
     }
-#ifdef RAE_ICACHE_TEST
-    }
-#endif
+    return acc;
+}
+
+template <int OPT>
+__device__ __forceinline__ void tile_apply(const StepArgs& a, float* M, float* aM, int nrows,
+                                           bool ones, int i0, int k0, int slot, rae_f4 acc,
+                                           const float pw[4], const float pa[4], int lane) {
+    const int li = lane & 15, lk = lane >> 4, col = k0 + li, m = a.m;
     float l1 = 0.f, l2 = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
@@ -132,6 +134,27 @@ __device__ void task_mfma_tile(const StepArgs& a, float* M, float* aM, int nrows
             a.regpart[2 * slot] = L1;
             a.regpart[2 * slot + 1] = L2;
         }
+    }
+}
+
+// One 16x16 tile per workgroup: the batch (K) split into four contiguous quarters, one per
+// wave, the four partial accumulators summed in wave order (deterministic) by wave 0, which
+// applies the update -- a K = L chain becomes four K = L/4 chains in parallel.
+template <int OPT>
+__device__ void wg_tile(const StepArgs& a, float* M, float* aM, int nrows, int odw, bool ones,
+                        int i0, int k0, int slot, int w, int lane, rae_f4* sacc) {
+    const int q = ((a.L + 15) / 16) * 4;                   // examples per wave, multiple of 4
+    const int b0 = min(w * q, a.L), b1 = min(b0 + q, a.L);
+    float pw[4], pa[4];
+    if (w == 0) tile_params<OPT>(a, M, aM, nrows, ones, i0, k0, lane, pw, pa);
+    const rae_f4 acc = tile_accum(a, nrows, odw, ones, i0, k0, b0, b1, lane);
+    sacc[w * RAE_WAVE + lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+        rae_f4 t = sacc[lane];
+#pragma unroll
+        for (int ww = 1; ww < RAE_NWAVE; ++ww) t += sacc[ww * RAE_WAVE + lane];
+        tile_apply<OPT>(a, M, aM, nrows, ones, i0, k0, slot, t, pw, pa, lane);
     }
 }
 
@@ -205,37 +228,22 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 // neg2), g(Ab[e]) = sum gamma_j.  Record metadata is loaded lane-parallel (one lane per
 // record) and broadcast with v_readlane (wave-uniform -> scalar addressing); the record
 // vectors are loaded UNR at a time with every load issued before the first FMA.
-template <int OPT, bool V4, int Q, bool XY>
-__device__ void task_entity_row(const StepArgs& a, int64_t slot, int x, int lane) {
+// entity_accum: records [st, en) of the slot's sorted list into g (lane-strided row) and gb
+// (this lane's share of the Ab gradient); rec0 = the record of a one-record row.
+template <bool V4, int Q, bool XY>
+__device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, int st, int en,
+                                             int rec0, RowVec<V4, Q>& g, float& gb, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
     constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
     typedef typename VecT<V4>::T VT;
-    const int r = a.r, nv = r / VW, s = a.s, NJ = 2 + 2 * s;
-    const int64_t base = slot * a.RA;
-    const int4 seg = reinterpret_cast<const int4*>(a.urowA)[base + x];   // row, start, end, rec0
-    const int e = seg.x, st = seg.y, en = seg.z;
-    float* prow = a.A + (int64_t)e * r;
-    float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
-    RowVec<V4, Q> pv, av, g;
-    pv.load(prow, nv, lane);                     // parameters in flight with the records
-    if (OPT == 0) av.load(arow, nv, lane); else av.zero();
-#ifdef RAE_STAMPS
-    if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
-        const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
-        a.stamps[(size_t)gw_ * 4 + 3] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-    const float ab0 = a.Ab[e];
-    const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
-    g.zero();
-    float gb = 0.f;
+    const int nv = a.r / VW, s = a.s, NJ = 2 + 2 * s;
     const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;   // SP: e2 has no A gradient (c = 0)
     const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
         // a one-record row's record rides in its segment: no srec round trip
-        const int rec = (en - st == 1) ? seg.w : a.srecA[base + c0 + (lane < n ? lane : 0)];
+        const int rec = (en - st == 1) ? rec0 : a.srecA[base + c0 + (lane < n ? lane : 0)];
         const int b = rec / NJ, j = rec - b * NJ;
         const int rb = b * a.lay.rec;
         const float* er = a.ex + rb + a.lay.ocoef + 2 * j;
@@ -276,45 +284,108 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int x, int lane
             for (int k0 = 0; k0 < n; k0 += UNRH) round(IntC<UNRH>{}, k0);
         }
     }
-    gb = wave_sum(gb);
-    apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
-    if (lane == 0) {
-        float ac = aab0;
-        a.Ab[e] = opt_update<OPT>(ab0, &ac, gb, a.lr);
-        if (OPT == 0) a.aAb[e] = ac;
-    }
 }
 
-// ---- W rows: g(W[f]) = sum over the row's CSR records of x_bf * dS_b ----------------------
-template <int OPT, bool V4, int Q>
-__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int x, int lane) {
+template <int OPT>
+__device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, float aab0, float gb) {
+    float ac = aab0;
+    a.Ab[e] = opt_update<OPT>(ab0, &ac, gb, a.lr);
+    if (OPT == 0) a.aAb[e] = ac;
+}
+
+__device__ __forceinline__ int4 row_segment(const StepArgs& a, int64_t slot, bool isA, int x) {
+    return isA ? reinterpret_cast<const int4*>(a.urowA)[slot * a.RA + x]    // row, start, end, rec0
+               : reinterpret_cast<const int4*>(a.urowW)[slot * a.RW + x];
+}
+
+template <int OPT, bool V4, int Q, bool XY>
+__device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int lane) {
     constexpr int VW = V4 ? 4 : 1;
-    constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
-    constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
-    typedef typename VecT<V4>::T VT;
-    const int m = a.m, nv = m / VW;
-    const int64_t base = slot * a.RW;
-    const int4 seg = reinterpret_cast<const int4*>(a.urowW)[base + x];   // row, start, end, rec0
-    const int f = seg.x, st = seg.y, en = seg.z;
-    const unsigned mask = (1u << a.posbits) - 1u;
-    float* prow = a.W + (int64_t)f * m;
-    float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
+    const int r = a.r, nv = r / VW;
+    const int64_t base = slot * a.RA;
+    const int e = seg.x;
+    float* prow = a.A + (int64_t)e * r;
+    float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
     RowVec<V4, Q> pv, av, g;
-    if (!a.reg_on) {
-        pv.load(prow, nv, lane);
-        if (OPT == 0) av.load(arow, nv, lane); else av.zero();
-    }
+    pv.load(prow, nv, lane);                     // parameters in flight with the records
+    if (OPT == 0) av.load(arow, nv, lane); else av.zero();
 #ifdef RAE_STAMPS
     if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
         const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
         a.stamps[(size_t)gw_ * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+    const float ab0 = a.Ab[e];
+    const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
     g.zero();
+    float gb = 0.f;
+    entity_accum<V4, Q, XY>(a, base, seg.y, seg.z, seg.w, g, gb, lane);
+    gb = wave_sum(gb);
+    apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+    if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb);
+}
+
+// A very heavy row (> RAE_VHEAVY records) per workgroup: its sorted record list split into
+// four contiguous chunks, one per wave; wave 0 sums the partial rows in wave order and applies
+// the update (its parameter loads in flight meanwhile).  spart: RAE_NWAVE * 64 * Q vectors.
+template <int OPT, bool V4, int Q, bool XY>
+__device__ void wg_entity_row(const StepArgs& a, int64_t slot, int x, int w, int lane,
+                              typename VecT<V4>::T* spart, float* sgb) {
+    constexpr int VW = V4 ? 4 : 1;
+    const int r = a.r, nv = r / VW;
+    const int64_t base = slot * a.RA;
+    const int4 seg = reinterpret_cast<const int4*>(a.vrowA)[slot * a.VCA + x];
+    const int e = seg.x, st = seg.y, en = seg.z;
+    const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
+    const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
+    float* prow = a.A + (int64_t)e * r;
+    float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
+    RowVec<V4, Q> pv, av, g;
+    float ab0 = 0.f, aab0 = 0.f;
+    if (w == 0) {
+        pv.load(prow, nv, lane);
+        if (OPT == 0) av.load(arow, nv, lane); else av.zero();
+        ab0 = a.Ab[e];
+        aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
+    }
+    g.zero();
+    float gb = 0.f;
+    if (c0 < c1) entity_accum<V4, Q, XY>(a, base, c0, c1, seg.w, g, gb, lane);
+    gb = wave_sum(gb);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) spart[(w * Q + q) * RAE_WAVE + lane] = g.v[q];
+    if (lane == 0) sgb[w] = gb;
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            g.v[q] = spart[q * RAE_WAVE + lane];
+#pragma unroll
+            for (int ww = 1; ww < RAE_NWAVE; ++ww) vadd(g.v[q], spart[(ww * Q + q) * RAE_WAVE + lane]);
+        }
+        float gt = sgb[0];
+#pragma unroll
+        for (int ww = 1; ww < RAE_NWAVE; ++ww) gt += sgb[ww];
+        apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+        if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gt);
+    }
+}
+
+// ---- W rows: g(W[f]) = sum over the row's CSR records of x_bf * dS_b ----------------------
+template <bool V4, int Q>
+__device__ __forceinline__ void feature_accum(const StepArgs& a, int64_t ex0, int64_t base,
+                                              int st, int en, int rec0, RowVec<V4, Q>& g,
+                                              int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
+    constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
+    typedef typename VecT<V4>::T VT;
+    const int nv = a.m / VW;
+    const unsigned mask = (1u << a.posbits) - 1u;
     const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
-        const unsigned rec = (unsigned)((en - st == 1) ? seg.w : a.srecW[base + c0 + (lane < n ? lane : 0)]);
+        const unsigned rec = (unsigned)((en - st == 1) ? rec0 : a.srecW[base + c0 + (lane < n ? lane : 0)]);
         const int b = (int)(rec >> a.posbits);
         float val = 1.f;
         if (a.values) val = a.values[a.indptr[ex0 + b] + (int)(rec & mask)];
@@ -347,6 +418,15 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
             for (int k0 = 0; k0 < n; k0 += UNRH) round(IntC<UNRH>{}, k0);
         }
     }
+}
+
+// W row f with gradient g: applied, or (lambda != 0) left in the dense scratch for k_dense_w
+template <int OPT, bool V4, int Q>
+__device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<V4, Q>& pv,
+                                               RowVec<V4, Q>& av, RowVec<V4, Q>& g, int lane) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int m = a.m, nv = m / VW;
     if (a.reg_on) {
         VT* gs = reinterpret_cast<VT*>(a.gWs + (int64_t)f * m);
 #pragma unroll
@@ -355,7 +435,62 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
             if (c < nv) gs[c] = g.v[q];
         }
     } else {
-        apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+        float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
+        apply_row<OPT, V4, Q>(a.W + (int64_t)f * m, arow, pv, av, g, nv, a.lr, lane);
+    }
+}
+
+template <int OPT, bool V4, int Q>
+__device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int4 seg, int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    const int m = a.m, nv = m / VW;
+    const int64_t base = slot * a.RW;
+    const int f = seg.x;
+    RowVec<V4, Q> pv, av, g;
+    if (!a.reg_on) {
+        pv.load(a.W + (int64_t)f * m, nv, lane);
+        if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
+    }
+#ifdef RAE_STAMPS
+    if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
+        const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
+        a.stamps[(size_t)gw_ * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    g.zero();
+    feature_accum<V4, Q>(a, ex0, base, seg.y, seg.z, seg.w, g, lane);
+    feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
+}
+
+// a very heavy W row per workgroup (as wg_entity_row)
+template <int OPT, bool V4, int Q>
+__device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int x, int w,
+                               int lane, typename VecT<V4>::T* spart) {
+    constexpr int VW = V4 ? 4 : 1;
+    const int m = a.m, nv = m / VW;
+    const int64_t base = slot * a.RW;
+    const int4 seg = reinterpret_cast<const int4*>(a.vrowW)[slot * a.VCW + x];
+    const int f = seg.x, st = seg.y, en = seg.z;
+    const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
+    const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
+    RowVec<V4, Q> pv, av, g;
+    if (w == 0 && !a.reg_on) {
+        pv.load(a.W + (int64_t)f * m, nv, lane);
+        if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
+    }
+    g.zero();
+    if (c0 < c1) feature_accum<V4, Q>(a, ex0, base, c0, c1, seg.w, g, lane);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) spart[(w * Q + q) * RAE_WAVE + lane] = g.v[q];
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            g.v[q] = spart[q * RAE_WAVE + lane];
+#pragma unroll
+            for (int ww = 1; ww < RAE_NWAVE; ++ww) vadd(g.v[q], spart[(ww * Q + q) * RAE_WAVE + lane]);
+        }
+        feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
     }
 }
 

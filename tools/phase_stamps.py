@@ -31,8 +31,9 @@ def build_diag():
         tag = VARIANT.replace("-D", "").replace("=", "").replace(" ", "_")
         DIAG = os.path.join(PKG, "rae", f"librae_hip_diag_{tag}.so")
     src = os.path.join(PKG, "csrc", "rae.hip")
-    if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < max(os.path.getmtime(s) for s in ge._sources()):
-        subprocess.run([ge.HIPCC, *ge.HIP_FLAGS, "-DRAE_STAMPS", *VARIANT.split(), src, "-o", DIAG],
+    _lib = ge._lib_mod()
+    if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < max(os.path.getmtime(s) for s in _lib.source_files()):
+        subprocess.run([ge.HIPCC, *_lib.BUILD_FLAGS, "-DRAE_STAMPS", *VARIANT.split(), src, "-o", DIAG],
                        check=True)
 
 
