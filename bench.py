@@ -85,14 +85,19 @@ def step_flops(L, l, m, r, dec):
 
 
 def pmc_traffic(config):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/), if any:
+    """L2-to-fabric (HBM + Infinity Cache) bytes per launch from the newest committed
+    rocprofv3 PMC passes (profiles/rNN_<config>_pmc_traffic.json), if any:
     2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half of a wide
-    coalesced read on gfx950), averaged over the launches of each kernel."""
-    path = os.path.join(ROOT, "profiles", f"r01_{config}_pmc_traffic.json")
-    if not os.path.exists(path):
+    coalesced read on gfx950; the same pass's rae_stream_copy, of known bytes, confirms the
+    factor), averaged over the launches of each kernel."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc_traffic.json")))
+    if not paths:
         return None
-    with open(path) as fh:
-        return json.load(fh)
+    with open(paths[-1]) as fh:
+        out = json.load(fh)
+    out["file"] = os.path.relpath(paths[-1], ROOT)
+    return out
 
 
 def _cpu_model():
@@ -338,7 +343,8 @@ def main():
                 "traffic": (traffic or {}).get(dom), "bytes_per_launch": kern[dom]["bytes_per_launch"],
                 "avg_launch_us": kern[dom]["avg_launch_us"],
                 "timing": TIMING,
-                "traffic_source": (traffic or {}).get("source")}
+                "traffic_source": ((traffic or {}).get("file", "") + ": " +
+                                   (traffic or {}).get("source", "")) if traffic else None}
     else:
         fl = step_flops(L, l, cfg["m"], cfg["r"], dec)
         pk = MFMA_BF16_PEAK_TFS if cfg.get("bf16") else MFMA_F32_PEAK_TFS
@@ -378,7 +384,16 @@ def main():
                  "avg_launch_us": lus, "bytes_per_launch": lbytes, "achieved": lach,
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": lach / HBM_PEAK_GBS,
                  "rows_per_s": Nl / (lus * 1e-6),
-                 "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label)"}
+                 "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label); "
+                          "no W-row reuse credited (SURVEY 8d) -- W (4dm bytes) is L2/MALL "
+                          "resident, so most of these bytes never reach HBM"}
+        lt = ((traffic or {}).get("per_kernel") or {}).get("rae::k_label")
+        if lt:
+            label["traffic"] = lt["traffic_bytes"]
+            label["traffic_GBs"] = lt["traffic_bytes"] / (lus * 1e-6) / 1e9
+            label["traffic_frac"] = label["traffic_GBs"] / HBM_PEAK_GBS
+            label["traffic_source"] = (f"{traffic.get('file')}: 2*FETCH_SIZE + WRITE_SIZE per "
+                                       f"launch (L2 misses: HBM and Infinity-Cache bytes)")
         del lab, pr
 
     # ---- measured copy bandwidth of this HBM: our own STREAM-style float4 copy kernel
@@ -408,6 +423,8 @@ def main():
                            "median of 7"}
         if label is not None:
             label["frac_of_measured_copy"] = label["achieved"] / hbm_copy["GBs"]
+            if "traffic_GBs" in label:
+                label["traffic_frac_of_measured_copy"] = label["traffic_GBs"] / hbm_copy["GBs"]
         roof["frac_of_measured_copy"] = (roof["achieved"] / hbm_copy["GBs"]
                                          if roof.get("unit") == "GB/s" else None)
         del src, dst

@@ -322,21 +322,24 @@ __global__ void k_finalize_cost(StepArgs a) {
     a.costs[batch] = (float)((double)*a.base_cost + (double)a.l1adj * L1 + (double)a.l2adj * L2);
 }
 
-// STREAM-style copy (measurement helper): 4 float4 loads in flight per lane before the stores
-__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ src,
-                                                     float4* __restrict__ dst, int64_t n) {
+// STREAM-style copy (measurement helper): 4 float4 nontemporal loads in flight per lane
+// before the stores, one 1024-vector block per workgroup -- the fastest of the forms
+// tools/probes/stream_probe.hip measured on MI355X (5.88 TB/s at 2 GiB)
+typedef float rae_v4f __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_copy(const rae_v4f* __restrict__ src,
+                                                     rae_v4f* __restrict__ dst, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * 1024;
     for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
-        float4 v[4];
+        rae_v4f v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t k = i + 256 * u;
-            v[u] = k < n ? src[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k < n) v[u] = __builtin_nontemporal_load(src + k);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t k = i + 256 * u;
-            if (k < n) dst[k] = v[u];
+            if (k < n) __builtin_nontemporal_store(v[u], dst + k);
         }
     }
 }
@@ -918,9 +921,9 @@ extern "C" int rae_stream_copy(const void* src, void* dst, int64_t bytes, rae_st
     const int64_t n = bytes / 16;
     if (n == 0) return RAE_OK;
     int64_t grid = (n + 1023) / 1024;
-    if (grid > 256 * 16) grid = 256 * 16;
+    if (grid > 65536) grid = 65536;
     hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
-                       (const float4*)src, (float4*)dst, n);
+                       (const rae_v4f*)src, (rae_v4f*)dst, n);
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }
