@@ -429,6 +429,32 @@ def main():
                                          if roof.get("unit") == "GB/s" else None)
         del src, dst
 
+    # ---- measured dense bf16 MFMA ceiling (rae_mfma_probe): the denominator next to the
+    # 2.5 PF datasheet label for the bilinear decoders' MFMA roofline
+    mfma_peak = None
+    if not args.no_label_pass:
+        blocks, iters = 256 * 8, 4096
+        sink = torch.empty(blocks * 4, dtype=torch.float32, device=dev)
+
+        def _mfma():
+            assert lib.rae_mfma_probe(iters, blocks, C.c_void_p(sink.data_ptr()), sp_) == 0, \
+                lib.rae_last_error()
+        _mfma()
+        torch.cuda.synchronize()
+        me = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(5)]
+        for a_, b_ in me:
+            a_.record(st)
+            _mfma()
+            b_.record(st)
+        torch.cuda.synchronize()
+        mus = float(np.median([a_.elapsed_time(b_) for a_, b_ in me]) * 1e3)
+        fl = blocks * 4.0 * iters * 8 * 16384
+        mfma_peak = {"TFLOPs": fl / (mus * 1e-6) / 1e12, "flops": fl, "us": mus,
+                     "how": "rae_mfma_probe: 2048 WGs x 4 waves, 8 independent "
+                            "v_mfma_f32_16x16x32_bf16 chains per wave, median of 5"}
+        if roof.get("unit") == "TFLOP/s" and cfg.get("bf16"):
+            roof["frac_of_measured_peak"] = roof["achieved"] / mfma_peak["TFLOPs"]
+
     ms_per_step = 1e3 * elapsed / K
     out = {
         "metric": METRIC,
@@ -457,6 +483,7 @@ def main():
                       "update_p50": float(np.median(upd_ms) * 1e3)},
         "label_pass": label,
         "hbm_copy": hbm_copy,
+        "mfma_bf16_peak": mfma_peak,
         "negative_sampling_s": t_neg,
         "negative_sampling": "host RandomState uniforms (reference stream) + device CDF search",
         "index_build_us_per_batch": index_us,

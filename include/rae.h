@@ -197,6 +197,10 @@ int rae_label(const int32_t* indptr, const int32_t* indices, const float* values
 /* STREAM-style device copy of `bytes` (multiple of 16, 16-byte aligned pointers) with float4
  * loads and stores: the measured HBM ceiling bench.py reports next to the 8 TB/s spec.   */
 int rae_stream_copy(const void* src_dev, void* dst_dev, int64_t bytes, rae_stream_t stream);
+/* bf16 MFMA throughput probe: `blocks` workgroups of 4 waves, each wave `iters` rounds of 8
+ * independent v_mfma_f32_16x16x32_bf16 (16384 flops each); writes one float per wave to
+ * sink_dev (blocks * 4 floats).  bench.py times it: the measured dense bf16 MFMA ceiling.  */
+int rae_mfma_probe(int64_t iters, int32_t blocks, float* sink_dev, rae_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,8 @@
 // Per training step (one func['train'] call of learning/OieInduction.py:189):
 //   SP:        k_forward  one workgroup per example: encoder + decoder forward/backward
 //                         (rae_sp.hpp) -> exchange record
-//   bilinear:  k_bil_enc -> k_bil_m (MFMA) -> k_bil_dec -> k_bil_dp (MFMA) -> k_bil_fin
+//   bilinear:  k_bil_enc -> k_bil_mt (MFMA) -> k_bil_dec -> k_bil_mt (MFMA) -> k_bil_dp (MFMA)
+//              -> k_bil_fin
 //                         (rae_bilinear.hpp) -> exchange record
 //   (the per-batch row index is built ahead, a window of batches at a time: k_build_index)
 //   [caller all-gathers the exchange records across data-parallel ranks]
@@ -54,15 +55,10 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
-__host__ __device__ inline int bil_m_tasks(int l, int r) {
-    return ((l + 15) / 16) * (int)(((int64_t)r * r + 63) / 64);
-}
-template <bool V4, bool BF16>
-__global__ __launch_bounds__(RAE_BT) void k_bil_m(StepArgs a) {
-    const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
-    if (t >= bil_m_tasks(a.l, a.r)) return;
-    if constexpr (BF16) bil_gemm_m_bf16(a, t, threadIdx.x & 63);
-    else bil_gemm_m<V4>(a, t, threadIdx.x & 63);
+template <bool BF16>
+__global__ __launch_bounds__(RAE_MTT) void k_bil_mt(StepArgs a, int pass) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bil_mt<BF16>(a, pass, smem);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_DBT) void k_bil_dec(StepArgs a) {
@@ -344,6 +340,31 @@ __global__ __launch_bounds__(256) void k_stream_copy(const rae_v4f* __restrict__
     }
 }
 
+// bf16 MFMA throughput probe (measurement helper): every wave runs `iters` rounds of 8
+// independent v_mfma_f32_16x16x32_bf16 chains (enough in flight to cover the dependent-issue
+// latency), operands in registers, one result per wave stored so nothing is dead code
+__global__ __launch_bounds__(256) void k_mfma_probe(int64_t iters, float* sink) {
+    typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    bf8 x, y;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        x[e] = (__bf16)(1e-3f * (float)((threadIdx.x + e) & 7));
+        y[e] = (__bf16)(1e-3f * (float)((threadIdx.x * 3 + e) & 7));
+    }
+    f4 acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc[c], 0, 0, 0);
+    }
+    float t = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) t += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+    if ((threadIdx.x & 63) == 0) sink[blockIdx.x * 4 + (threadIdx.x >> 6)] = t;
+}
+
 __global__ void k_add_cursor(int64_t* cursor, int64_t count) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *cursor += count;
 }
@@ -378,6 +399,8 @@ struct rae_plan {
     size_t smem_fwd = 0;
     size_t smem_idx = 0;
     size_t smem_dec = 0;
+    size_t smem_mt = 0;     // k_bil_mt: one 16 x 16 x m block of R in LDS
+    bool mt_bf16 = false;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
     int q = 1;
@@ -568,8 +591,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         else if (c.embed <= 256 && c.relations <= 128) p->dp2 = 2;
     }
     a.nib = bil ? (p->dp2 ? (c.embed + RAE_IB2 - 1) / RAE_IB2 : (c.embed + RAE_IB - 1) / RAE_IB) : 0;
-    const size_t o_mbuf = bil ? take(4ull * c.batch_size * c.embed * c.embed) : 0;
     const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
+    a.r4 = align4(c.embed);
+    const int64_t nbi_mt = (c.embed + RAE_MTI - 1) / RAE_MTI, nbj_mt = (c.embed + RAE_MTJ - 1) / RAE_MTJ;
+    const size_t o_mtv = bil ? take(4ull * nbj_mt * c.batch_size * a.r4) : 0;
+    const size_t o_mtw = bil ? take(4ull * nbi_mt * c.batch_size * a.r4) : 0;
     a.Lp = (L + 31) / 32 * 32;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
@@ -596,8 +622,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.desc = reinterpret_cast<int32_t*>(p->ws + o_desc);
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
-    a.Mbuf = bil ? reinterpret_cast<float*>(p->ws + o_mbuf) : nullptr;
     a.dPpart = bil ? reinterpret_cast<float*>(p->ws + o_dpp) : nullptr;
+    a.mtV = bil ? reinterpret_cast<float*>(p->ws + o_mtv) : nullptr;
+    a.mtW = bil ? reinterpret_cast<float*>(p->ws + o_mtw) : nullptr;
     a.facT = a.bf16 ? reinterpret_cast<float*>(p->ws + o_fac) : nullptr;
     a.pfrag = a.bf16 ? reinterpret_cast<uint4*>(p->ws + o_pfr) : nullptr;
     a.err = p->d_err;
@@ -608,7 +635,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP;
     p->smem_fwd = smem_ex;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
-    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024) {
+    // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
+    p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
+    p->smem_mt = bil ? bil_mt_lds_bytes(c.relations, p->mt_bf16) : 0;
+    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024 ||
+        p->smem_mt > 160 * 1024) {
         (void)hipFree(p->ws);
         delete p;
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
@@ -635,6 +666,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<7, 7>());
             (void)hipFuncSetAttribute((const void*)k_bil_dp2<8, 8>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<8, 8>());
+            (void)hipFuncSetAttribute((const void*)k_bil_mt<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
+            (void)hipFuncSetAttribute((const void*)k_bil_mt<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
             (void)hipFuncSetAttribute((const void*)k_bil_dec<true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
             (void)hipFuncSetAttribute((const void*)k_bil_dec<false>,
@@ -697,12 +732,12 @@ template <bool V4>
 static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
     RAE_LAUNCH(p, (k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
-    const int gm = ceil_div(bil_m_tasks(a.l, a.r), RAE_NWAVE);
-    if (V4 && a.bf16)
-        RAE_LAUNCH(p, (k_bil_m<V4, true>), dim3(gm), dim3(RAE_BT), 0, st, a);
-    else
-        RAE_LAUNCH(p, (k_bil_m<V4, false>), dim3(gm), dim3(RAE_BT), 0, st, a);
+    const dim3 gmt(((a.r + RAE_MTI - 1) / RAE_MTI) * ((a.r + RAE_MTJ - 1) / RAE_MTJ));
+    if (p->mt_bf16) RAE_LAUNCH(p, k_bil_mt<true>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 0);
+    else RAE_LAUNCH(p, k_bil_mt<false>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 0);
     RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
+    if (p->mt_bf16) RAE_LAUNCH(p, k_bil_mt<true>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
+    else RAE_LAUNCH(p, k_bil_mt<false>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
     const size_t lds77 = dp2_lds_bytes<7, 7>(), lds88 = dp2_lds_bytes<8, 8>();
     if (p->dp2 == 1)
@@ -924,6 +959,14 @@ extern "C" int rae_stream_copy(const void* src, void* dst, int64_t bytes, rae_st
     if (grid > 65536) grid = 65536;
     hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
                        (const rae_v4f*)src, (rae_v4f*)dst, n);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+
+extern "C" int rae_mfma_probe(int64_t iters, int32_t blocks, float* sink, rae_stream_t stream) {
+    if (!sink || iters < 1 || blocks < 1) return fail(RAE_E_INVALID, "bad argument");
+    hipLaunchKernelGGL(k_mfma_probe, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       iters, sink);
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }

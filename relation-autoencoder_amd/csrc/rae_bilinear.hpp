@@ -15,15 +15,21 @@
 //   dA[e1] = dOne M a2 + M y,  dA[e2] = M^T x,  dA[n1_t] = dg1_t M a2,  dA[n2_t] = dg2_t M^T a1
 //   (+ the SP terms for the hybrid).
 //
-// The forward phase of one step is five launches (all over this rank's l examples):
+// The forward phase of one step is six launches (all over this rank's l examples); M_b is
+// never materialised (SURVEY 7 hard part v):
 //   k_bil_enc  per example : encoder (P, log P, H), hybrid wC1/wC2, copies of A[e1], A[e2]
-//   k_bil_m    MFMA GEMM   : M[b][i*r+j] = sum_k P[b][k] R[i][j][k]   (l x r^2, K = m)
-//   k_bil_dec  per example : M a2, M^T a1 (one sweep of M_b), scores, loss, x, y,
-//                            M y, M^T x (second sweep), the A-row gradient vectors
+//   k_bil_mt   MFMA pass   : one workgroup per 8 x 16 block of R's (i, j), staged in LDS; the
+//                            block's M tiles M_b[i][j] = sum_k P_bk R[i][j][k] (K = m)
+//                            contracted at once both ways: partials of M a2 and M^T a1
+//   k_bil_dec  per example : v = M a2, w = M^T a1 (partials summed), scores, loss,
+//                            coefficients, x, y (+ hybrid dw1, dw2)
+//   k_bil_mt   again       : partials of M y, M^T x
 //   k_bil_dp   MFMA GEMM   : dP partials  sum_{i in block} sum_j U[b][i,j] R[i][j][k],
 //                            U = x a2^T + a1 y^T generated on the fly (split over i-blocks)
-//   k_bil_fin  per example : dP (+ hybrid C^T dw) -> entropy + softmax backward -> dS
-// All GEMMs run on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).
+//   k_bil_fin  per example : dP (+ hybrid C^T dw) -> entropy + softmax backward -> dS; the
+//                            A-row gradient vectors from v, w, M y, M^T x
+// The GEMMs run on v_mfma_f32_16x16x4_f32 (exact fp32) or, with rae_config.mfma_bf16 (BASELINE
+// config 5), on v_mfma_f32_16x16x32_bf16 (bf16 operands, fp32 accumulation).
 #pragma once
 #include "rae_common.hpp"
 #include "rae_sp.hpp"
@@ -33,9 +39,8 @@ namespace rae {
 
 typedef float rae_bf4 __attribute__((ext_vector_type(4)));
 #define RAE_IB 8     // i rows per dP partial block (k_bil_dp)
+#ifndef RAE_KG
 #define RAE_KG 8     // 16-column tiles of m per pass of one R-row task (task_bilinear_rows)
-#ifndef RAE_SWEEP_RB
-#define RAE_SWEEP_RB 4   // M_b rows per wave whose loads are in flight together (bil_sweep)
 #endif
 
 // ---- k_bil_enc: encoder + hybrid SP projections --------------------------------------------
@@ -72,78 +77,10 @@ __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];     // H until k_bil_dec
 }
 
-// ---- k_bil_m: M[b][ij] = sum_k P[b][k] R[ij][k]  (one wave = 16 examples x 64 ij) ----------
-// MFMA 16x16x4: A[b][kk] = P, B[kk][ij] = R, D[b][ij]; with V4 the four K-slots of a lane
-// take 4 consecutive k (one float4 per operand row per 4 MFMAs).
-template <bool V4>
-__device__ void bil_gemm_m(const StepArgs& a, int t, int lane) {
-    const int l = a.l, m = a.m, r = a.r;
-    const int nbt = (l + 15) / 16;
-    const int64_t rr = (int64_t)r * r;
-    const int bt = t % nbt;
-    const int64_t ij0 = (int64_t)(t / nbt) * 64;
-    const int li = lane & 15, kk = lane >> 4;
-    const int b = bt * 16 + li;
-    const bool bv = b < l;
-    const float* Prow = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec + a.lay.oP;
-    const float* Rrow[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int64_t ij = ij0 + 16 * n + li;
-        Rrow[n] = a.R3 + (ij < rr ? ij : rr - 1) * m;
-    }
-    rae_bf4 acc[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (V4) {
-        for (int k0 = 0; k0 < m; k0 += 16) {
-            const int k = k0 + 4 * kk;
-            const bool kv = k < m;                  // m % 4 == 0: the whole float4 is valid
-            const int kc = kv ? k : 0;
-            float4 p = *reinterpret_cast<const float4*>(Prow + kc);
-            if (!kv || !bv) p = make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 rv[4];
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                rv[n] = *reinterpret_cast<const float4*>(Rrow[n] + kc);
-                if (!kv) rv[n] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(p.x, rv[n].x, acc[n], 0, 0, 0);
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(p.y, rv[n].y, acc[n], 0, 0, 0);
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(p.z, rv[n].z, acc[n], 0, 0, 0);
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(p.w, rv[n].w, acc[n], 0, 0, 0);
-            }
-        }
-    } else {
-        for (int k0 = 0; k0 < m; k0 += 4) {
-            const int k = k0 + kk;
-            const bool kv = k < m;
-            const int kc = kv ? k : 0;
-            const float p = (kv && bv) ? Prow[kc] : 0.f;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const float rv = kv ? Rrow[n][kc] : 0.f;
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, rv, acc[n], 0, 0, 0);
-            }
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int64_t ij = ij0 + 16 * n + li;
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int bo = bt * 16 + kk * 4 + reg;
-            if (bo < l && ij < rr) a.Mbuf[(int64_t)bo * rr + ij] = acc[n][reg];
-        }
-    }
-}
-
-// ---- bf16-operand forms (rae_config.mfma_bf16; BASELINE config 5) ------------------------
+// ---- bf16 fragments -----------------------------------------------------------------------
 // v_mfma_f32_16x16x32_bf16: lane l holds A[l&15][8(l>>4) + e] and B[8(l>>4) + e][l&15],
-// e = 0..7; fp32 values are rounded to bf16 (v_cvt_pk_bf16_f32, nearest even) as they enter
-// the fragment, accumulation stays fp32.  K = 32 per instruction instead of 4.
+// e = 0..7; fp32 values are rounded to bf16 (nearest even) as they enter the fragment,
+// accumulation stays fp32.  K = 32 per instruction instead of 4.
 typedef __bf16 rae_bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
@@ -153,53 +90,206 @@ __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
     return v;
 }
 
-// M[b][ij] (as bil_gemm_m) with bf16 operands; m % 4 == 0
-__device__ void bil_gemm_m_bf16(const StepArgs& a, int t, int lane) {
-    const int l = a.l, m = a.m, r = a.r;
-    const int nbt = (l + 15) / 16;
-    const int64_t rr = (int64_t)r * r;
-    const int bt = t % nbt;
-    const int64_t ij0 = (int64_t)(t / nbt) * 64;
+// ---- k_bil_mt: M-tile passes over R blocks, M never stored ---------------------------------
+// Workgroup (it, jt) stages the block R[i0..i0+7][j0..j0+15][0..m) in LDS (fp32, or bf16 with
+// K padded to 32: every (i, j) row of k is one fragment run).  Each wave takes 16-example
+// tiles; for every i of the block one MFMA chain (K = m) gives the transposed M tile
+//   D[j][b] = sum_k R[i][j][k] P_bk = M_b[i][j]        (A = the block's rows j at this i,
+//                                                       B = P^T: lane (li, g) holds
+//                                                       D[j0 + 4g + reg][b0 + li])
+// which is contracted at once, both ways, with the example's vectors:
+//   cv side:  vpart[jt][b][i] = sum_{j in block} D[j][b] cv_b[j]      (cv = a2, pass 1; y, pass 2)
+//   cw side:  wpart[it][b][j] = sum_{i in block} cw_b[i] D[j][b]      (cw = a1, pass 1; x, pass 2)
+// Partials per j-block / i-block are summed in block order by the consumer (k_bil_dec for
+// pass 1: v = M a2, w = M^T a1; k_bil_fin for pass 2: M y, M^T x) -- deterministic.  R is read
+// once per pass; (r/8)(r/16) workgroups (325 at r = 200: every block's staging in one round).
+#define RAE_MTI 8         // rows i per block
+#define RAE_MTJ 16        // columns j per block (one MFMA tile of rows)
+#define RAE_MTT RAE_FBT   // threads per k_bil_mt workgroup (8 waves)
+#define RAE_MTW (RAE_MTT / RAE_WAVE)
+#define RAE_MT_SB 8       // float4 staging loads per thread in flight per round
+__host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
+    const int KP = (m + 31) / 32 * 32;
+    return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 : (size_t)RAE_MTI * RAE_MTJ * m * 4;
+}
+#ifdef RAE_STAMPS      // pass 0 only, past the per-example stamp region (l <= 1024)
+#define RAE_MT_STAMP(slot)                                                                      \
+    do {                                                                                        \
+        if (a.stamps && pass == 0 && threadIdx.x == 0)                                          \
+            a.stamps[16384 + (size_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define RAE_MT_STAMP(slot) do { } while (0)
+#endif
+
+template <bool BF16>
+__device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
+    const int r = a.r, m = a.m, l = a.l;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, g = lane >> 4;
-    const int b = bt * 16 + li;
-    const bool bv = b < l;
-    const float* Prow = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec + a.lay.oP;
-    const float* Rrow[4];
+    const int nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
+    const int it = blockIdx.x / nbj, jt = blockIdx.x - it * nbj;
+    const int i0 = it * RAE_MTI, j0 = jt * RAE_MTJ;
+    const int KP = (m + 31) / 32 * 32, ST = BF16 ? KP + 8 : m;   // row (i, j) stride in LDS
+    RAE_MT_STAMP(0);
+    // ---- stage: LDS row (ii, jj) = R[i0+ii][j0+jj][0..m); rows past r are zero
+    if ((m & 3) == 0) {
+        const int m4 = m / 4, nv = RAE_MTI * RAE_MTJ * m4;
+        for (int e0 = 0; e0 < nv; e0 += RAE_MTT * RAE_MT_SB) {
+            float4 v[RAE_MT_SB];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int64_t ij = ij0 + 16 * n + li;
-        Rrow[n] = a.R3 + (ij < rr ? ij : rr - 1) * m;
-    }
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    rae_bf4 acc[4];
+            for (int u = 0; u < RAE_MT_SB; ++u) {
+                const int e = e0 + u * RAE_MTT + tid;
+                const int row = e / m4, kq = e - row * m4;
+                const int i = i0 + row / RAE_MTJ, j = j0 + row % RAE_MTJ;
+                const bool ok = e < nv && i < r && j < r;
+                const float4 x = *reinterpret_cast<const float4*>(
+                    a.R3 + ((int64_t)(ok ? i : 0) * r + (ok ? j : 0)) * m + 4 * kq);
+                v[u] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < m; k0 += 32) {
-        const int ka = k0 + 8 * g, kb = ka + 4;
-        const bool va = ka < m, vb = kb < m;
-        float4 p0 = *reinterpret_cast<const float4*>(Prow + (va ? ka : 0));
-        float4 p1 = *reinterpret_cast<const float4*>(Prow + (vb ? kb : 0));
-        if (!va || !bv) p0 = z4;
-        if (!vb || !bv) p1 = z4;
-        const rae_bf16x8 pa = to_bf16x8(p0, p1);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            float4 r0 = *reinterpret_cast<const float4*>(Rrow[n] + (va ? ka : 0));
-            float4 r1 = *reinterpret_cast<const float4*>(Rrow[n] + (vb ? kb : 0));
-            if (!va) r0 = z4;
-            if (!vb) r1 = z4;
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, to_bf16x8(r0, r1), acc[n], 0, 0, 0);
+            for (int u = 0; u < RAE_MT_SB; ++u) {
+                const int e = e0 + u * RAE_MTT + tid;
+                if (e < nv) {
+                    const int row = e / m4, kq = e - row * m4;
+                    if constexpr (BF16) {
+                        typedef __bf16 bf4_t __attribute__((ext_vector_type(4)));
+                        bf4_t q;
+                        q[0] = (__bf16)v[u].x; q[1] = (__bf16)v[u].y;
+                        q[2] = (__bf16)v[u].z; q[3] = (__bf16)v[u].w;
+                        *reinterpret_cast<bf4_t*>(reinterpret_cast<__bf16*>(smem) + row * ST + 4 * kq) = q;
+                    } else {
+                        *reinterpret_cast<float4*>(reinterpret_cast<float*>(smem) + row * ST + 4 * kq) = v[u];
+                    }
+                }
+            }
+        }
+    } else {
+        for (int e = tid; e < RAE_MTI * RAE_MTJ * m; e += RAE_MTT) {
+            const int row = e / m, k = e - row * m;
+            const int i = i0 + row / RAE_MTJ, j = j0 + row % RAE_MTJ;
+            const float x = (i < r && j < r) ? a.R3[((int64_t)i * r + j) * m + k] : 0.f;
+            if constexpr (BF16) reinterpret_cast<__bf16*>(smem)[row * ST + k] = (__bf16)x;
+            else reinterpret_cast<float*>(smem)[row * ST + k] = x;
         }
     }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int64_t ij = ij0 + 16 * n + li;
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int bo = bt * 16 + g * 4 + reg;
-            if (bo < l && ij < rr) a.Mbuf[(int64_t)bo * rr + ij] = acc[n][reg];
+    if constexpr (BF16) {                      // zero K padding [m, KP)
+        for (int e = tid; e < RAE_MTI * RAE_MTJ * (KP - m); e += RAE_MTT) {
+            const int row = e / (KP - m), k = m + (e - row * (KP - m));
+            reinterpret_cast<__bf16*>(smem)[row * ST + k] = (__bf16)0.f;
         }
     }
+    RAE_MT_STAMP(1);
+    const int ov = pass == 0 ? a.lay.oA2 : a.lay.oY;      // cv: contracted over j
+    const int ow = pass == 0 ? a.lay.oA1 : a.lay.oX;      // cw: contracted over i
+    const int nbt = (l + 15) / 16;
+    bool first = true;
+    for (int bt = w; bt < nbt || first; bt += RAE_MTW) {
+        const bool has = bt < nbt;
+        // operands of this lane's example b0 + li, loaded before the barrier (in flight with
+        // the staging): P (the B fragments), cv at j0 + 4g .. +3, cw at i0 .. i0 + 7
+        const int bb = bt * 16 + li;
+        const bool bv = has && bb < l;
+        const float* erb = a.ex + (int64_t)(a.rank * l + (bv ? bb : 0)) * a.lay.rec;
+        const float* Pa = erb + a.lay.oP;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 cv = *reinterpret_cast<const float4*>(erb + ov + (j0 + 4 * g < r ? j0 + 4 * g : 0));
+        if (!bv || j0 + 4 * g >= r) cv = z4;
+        float cw[RAE_MTI];
+#pragma unroll
+        for (int q = 0; q < RAE_MTI / 4; ++q) {
+            const int i = i0 + 4 * q;
+            const float4 c = *reinterpret_cast<const float4*>(erb + ow + (i < r ? i : 0));
+            const bool ok = bv && i < r;
+            cw[4 * q + 0] = ok ? c.x : 0.f; cw[4 * q + 1] = ok ? c.y : 0.f;
+            cw[4 * q + 2] = ok ? c.z : 0.f; cw[4 * q + 3] = ok ? c.w : 0.f;
+        }
+        rae_bf16x8 pf[4];                            // bf16: K <= 128 (m <= 128)
+        if constexpr (BF16) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int k0 = ks * 32 + 8 * g;
+                const float4 lo = *reinterpret_cast<const float4*>(Pa + (k0 < m ? k0 : 0));
+                const float4 hi = *reinterpret_cast<const float4*>(Pa + (k0 + 4 < m ? k0 + 4 : 0));
+                pf[ks] = to_bf16x8((bv && k0 < m) ? lo : z4, (bv && k0 + 4 < m) ? hi : z4);
+            }
+        }
+        if (first) {
+            RAE_MT_STAMP(2);
+            __syncthreads();                         // the block is staged
+            RAE_MT_STAMP(3);
+            first = false;
+        }
+        if (!has) break;
+        float vp[RAE_MTI];                           // cv side, per i of the block
+        float4 wacc = z4;                            // cw side: j0 + 4g + reg
+#pragma unroll
+        for (int ii = 0; ii < RAE_MTI; ++ii) {
+            rae_bf4 acc = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (BF16) {
+                const __bf16* srow = reinterpret_cast<const __bf16*>(smem) + (ii * RAE_MTJ + li) * ST + 8 * g;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    if (ks * 32 < KP) {
+                        const rae_bf16x8 sf = *reinterpret_cast<const rae_bf16x8*>(srow + ks * 32);
+                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sf, pf[ks], acc, 0, 0, 0);
+                    }
+                }
+            } else {
+                const float* srow = reinterpret_cast<const float*>(smem) + (ii * RAE_MTJ + li) * ST;
+                for (int k0 = 0; k0 < m; k0 += 4) {
+                    const int k = k0 + g;
+                    const float sa = k < m ? srow[k] : 0.f;
+                    const float pb = (bv && k < m) ? Pa[k] : 0.f;
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, pb, acc, 0, 0, 0);
+                }
+            }
+            vp[ii] = acc[0] * cv.x + acc[1] * cv.y + acc[2] * cv.z + acc[3] * cv.w;
+            wacc.x += cw[ii] * acc[0];
+            wacc.y += cw[ii] * acc[1];
+            wacc.z += cw[ii] * acc[2];
+            wacc.w += cw[ii] * acc[3];
+        }
+        RAE_MT_STAMP(4);
+        // cv side: sum over the four lane groups g (fixed order); groups 0, 1 write i0 + 4g..+3
+#pragma unroll
+        for (int ii = 0; ii < RAE_MTI; ++ii) {
+            vp[ii] += __uint_as_float(xor16_u32(__float_as_uint(vp[ii])));
+            vp[ii] += __uint_as_float(xor32_u32(__float_as_uint(vp[ii])));
+        }
+        if (bv) {
+            float* vo = a.mtV + ((int64_t)jt * l + bb) * a.r4 + i0 + 4 * g;
+            if (g < 2 && i0 + 4 * g < r) {
+                float4 o;
+                o.x = g == 0 ? vp[0] : vp[4];
+                o.y = g == 0 ? vp[1] : vp[5];
+                o.z = g == 0 ? vp[2] : vp[6];
+                o.w = g == 0 ? vp[3] : vp[7];
+                *reinterpret_cast<float4*>(vo) = o;
+            }
+            if (j0 + 4 * g < r)
+                *reinterpret_cast<float4*>(a.mtW + ((int64_t)it * l + bb) * a.r4 + j0 + 4 * g) = wacc;
+        }
+        RAE_MT_STAMP(5);
+    }
+}
+
+// sum of the per-block partials of one example's M-tile output (four interleaved chains, a
+// fixed order: the loads are independent)
+__device__ __forceinline__ float mt_sum(const float* part, int nblk, int l, int r4, int b, int i) {
+    const float* p = part + (int64_t)b * r4 + i;
+    const int64_t st = (int64_t)l * r4;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    int q = 0;
+    for (; q + 4 <= nblk; q += 4) {
+        t0 += p[q * st];
+        t1 += p[(q + 1) * st];
+        t2 += p[(q + 2) * st];
+        t3 += p[(q + 3) * st];
+    }
+    for (; q < nblk; ++q) t0 += p[q * st];
+    return (t0 + t1) + (t2 + t3);
 }
 
 // dP partials (as bil_gemm_dp) with bf16 operands; K = j in steps of 32
@@ -405,8 +495,7 @@ __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
 }
 
 // ---- k_bil_dec helpers ----------------------------------------------------------------------
-// k_bil_dec runs 16 waves per example (RAE_DBT threads), twice the forward kernels' 8: the two
-// M_b sweeps are bound by how many loads each CU has in flight (C5 forward 79.3 -> 73.8 us)
+// k_bil_dec runs 16 waves per example (RAE_DBT threads): the 2s negative rows' gathers and dots
 #ifndef RAE_DBT
 #define RAE_DBT 1024
 #endif
@@ -440,72 +529,7 @@ __device__ inline BilSmem carve_bil_smem(char* smem, int r, int s) {
     return S;
 }
 
-// One pass over M_b (r x r, row-major in HBM):
-//   row_out[i] = sum_j M[i][j] vr[j]        col_out[j] = sum_i vl[i] M[i][j]
-// wave w takes rows i = w, w + NW, ...; lanes hold column vectors; the column sums are
-// per-wave partials combined in wave order (deterministic).
-template <bool V4>
-__device__ void bil_sweep(const float* M, int r, const float* vr, const float* vl, float* row_out,
-                          float* col_out, float* part) {
-    typedef typename VecT<V4>::T VT;
-    constexpr int VW = V4 ? 4 : 1;
-    constexpr int RB = RAE_SWEEP_RB;
-    const int rv = r / VW, r4 = align4(r);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const VT* vrv = reinterpret_cast<const VT*>(vr);
-    VT cacc[2], vrc[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        vzero(cacc[q]);
-        const int c = lane + 64 * q;
-        if (c < rv) vrc[q] = vrv[c]; else vzero(vrc[q]);
-    }
-    for (int i0 = w; i0 < r; i0 += RAE_DNW * RB) {
-        VT x[RB][2];
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int i = min(i0 + RAE_DNW * u, r - 1);
-            const VT* Mi = reinterpret_cast<const VT*>(M + (int64_t)i * r);
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int c = lane + 64 * q;
-                x[u][q] = Mi[c < rv ? c : 0];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int i = i0 + RAE_DNW * u;
-            const bool iv = i < r;
-            const float li = iv ? vl[i] : 0.f;
-            float d = 0.f;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int c = lane + 64 * q;
-                if (c < rv) {
-                    d += vdot(x[u][q], vrc[q]);
-                    vfma(cacc[q], li, x[u][q]);
-                }
-            }
-            d = wave_sum(d);
-            if (iv && lane == 0) row_out[i] = d;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int c = lane + 64 * q;
-        if (c < rv) reinterpret_cast<VT*>(part + w * r4)[c] = cacc[q];
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < r; j += RAE_DBT) {
-        float t = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < RAE_DNW; ++ww) t += part[ww * r4 + j];
-        col_out[j] = t;
-    }
-    __syncthreads();
-}
-
-// ---- k_bil_dec: scores, loss, coefficients, A-row gradient vectors -----------------------
+// ---- k_bil_dec: scores, loss, coefficients, x, y -----------------------
 template <bool V4>
 __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     typedef typename VecT<V4>::T VT;
@@ -542,14 +566,28 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     const float H = rec[a.lay.oloss];
     __syncthreads();
     RAE_STAMP(a, 1);
-    // negative rows: rows[t] = A[n1_t], rows[s + t] = A[n2_t]
+    // negative rows: rows[t] = A[n1_t], rows[s + t] = A[n2_t]; v = M a2, w = M^T a1: the
+    // first k_bil_mt pass's block partials, summed in block order
     for (int e = threadIdx.x; e < 2 * s * rv; e += RAE_DBT) {
         const int t = e / rv, c = e - t * rv;
         const VT* src = reinterpret_cast<const VT*>(a.A + (int64_t)S.ids[2 + t] * r);
         reinterpret_cast<VT*>(S.rows)[t * r4v + c] = src[c];
     }
-    const float* Mb = a.Mbuf + (int64_t)bl * r * r;
-    bil_sweep<V4>(Mb, r, S.a2, S.a1, S.v, S.w, S.part);     // v = M a2, w = M^T a1 (+ barrier)
+    {
+        const int nbi = (r + RAE_MTI - 1) / RAE_MTI, nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
+        for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
+            const bool iv = i < r;
+            const float v = iv ? mt_sum(a.mtV, nbj, a.l, a.r4, bl, i) : 0.f;
+            const float w = iv ? mt_sum(a.mtW, nbi, a.l, a.r4, bl, i) : 0.f;
+            S.v[i] = v;
+            S.w[i] = w;
+            if (iv) {
+                rec[a.lay.oG1 + i] = v;                   // for k_bil_fin
+                rec[a.lay.oG2 + i] = w;
+            }
+        }
+    }
+    __syncthreads();
     RAE_STAMP(a, 2);
 
     // dot products: rho < s: n1_t.(v [+ wC1]); s <= rho < 2s: n2_t.(w [+ wC2]);
@@ -622,46 +660,32 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
     }
     __syncthreads();
 
-    // x = dOne a1 + sum_t dg1_t n1_t ; y = sum_t dg2_t n2_t ; hybrid dw1/dw2 (sums in t order)
+    // x = dOne a1 + sum_t dg1_t n1_t ; y = sum_t dg2_t n2_t ; hybrid dw1/dw2 (sums in t order),
+    // straight into the record (the second k_bil_vw pass and k_bil_dp read x, y from there)
     {
         const float dOne = S.red[0], ca1 = S.red[1], ca2 = S.red[2];
-        for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
+        for (int i = threadIdx.x; i < r; i += RAE_DBT) {
             float n1 = 0.f, n2 = 0.f;
             for (int t = 0; t < s; ++t) {
                 n1 += S.coef[3 * (2 + t)] * S.rows[t * r4 + i];
                 n2 += S.coef[3 * (2 + s + t) + 1] * S.rows[(s + t) * r4 + i];
             }
-            const bool iv = i < r;
-            S.x[i] = iv ? dOne * S.a1[i] + n1 : 0.f;
-            S.y[i] = iv ? n2 : 0.f;
-            S.dw1[i] = iv ? ca1 * S.a1[i] + n1 : 0.f;
-            S.dw2[i] = iv ? ca2 * S.a2[i] + n2 : 0.f;
-        }
-    }
-    __syncthreads();
-    RAE_STAMP(a, 4);
-    bil_sweep<V4>(Mb, r, S.y, S.x, S.My, S.Mtx, S.part);    // M y, M^T x
-    RAE_STAMP(a, 5);
-
-    {
-        const float dOne = S.red[0], ca1 = S.red[1], ca2 = S.red[2];
-        for (int i = threadIdx.x; i < r; i += RAE_DBT) {
-            const float c1 = hybrid ? S.wC1[i] : 0.f, c2 = hybrid ? S.wC2[i] : 0.f;
-            rec[a.lay.oV1 + i] = S.v[i] + c1;
-            rec[a.lay.oV2 + i] = S.w[i] + c2;
-            rec[a.lay.oG1 + i] = dOne * S.v[i] + S.My[i] + ca1 * c1;
-            rec[a.lay.oG2 + i] = S.Mtx[i] + ca2 * c2;
-            rec[a.lay.oX + i] = S.x[i];
-            rec[a.lay.oY + i] = S.y[i];
-            rec[a.lay.odw1 + i] = hybrid ? S.dw1[i] : 0.f;
-            rec[a.lay.odw2 + i] = hybrid ? S.dw2[i] : 0.f;
+            rec[a.lay.oX + i] = dOne * S.a1[i] + n1;
+            rec[a.lay.oY + i] = n2;
+            rec[a.lay.odw1 + i] = hybrid ? ca1 * S.a1[i] + n1 : 0.f;
+            rec[a.lay.odw2 + i] = hybrid ? ca2 * S.a2[i] + n2 : 0.f;
         }
         for (int j = threadIdx.x; j < NJ; j += RAE_DBT) {
             const float* c = S.coef + 3 * j;
             rec[a.lay.ocoef + 2 * j] = j < 2 ? 1.f : (j < 2 + s ? c[0] : c[1]);
             rec[a.lay.ocoef + 2 * j + 1] = c[2];
         }
-        if (threadIdx.x == 0) rec[a.lay.oloss] = S.red[32];
+        if (threadIdx.x == 0) {
+            rec[a.lay.oloss] = S.red[32];
+            rec[a.lay.oAux + 0] = dOne;
+            rec[a.lay.oAux + 1] = ca1;
+            rec[a.lay.oAux + 2] = ca2;
+        }
     }
     RAE_STAMP(a, 6);
 }
@@ -743,6 +767,21 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
     sz = block_sum<RAE_BT>(sz, red + RAE_NWAVE);
     for (int k = threadIdx.x; k < m; k += RAE_BT)
         rec[a.lay.odS + k] = rec[a.lay.oP + k] * ((sdp[k] - sd) + ce * (rec[a.lay.oZ + k] - sz));
+    // the A-row gradient vectors (rae_step.hpp), from v = M a2, w = M^T a1 (record G1 / G2),
+    // M y, M^T x (My / MtX) and the hybrid's wC1 / wC2 (V1 / V2):
+    //   V1 = v + wC1,  V2 = w + wC2,  G1 = dOne v + M y + c_a1 wC1,  G2 = M^T x + c_a2 wC2
+    const float dOne = rec[a.lay.oAux + 0], ca1 = rec[a.lay.oAux + 1], ca2 = rec[a.lay.oAux + 2];
+    const int nbi = (r + RAE_MTI - 1) / RAE_MTI, nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
+    for (int i = threadIdx.x; i < r; i += RAE_BT) {
+        const float v = rec[a.lay.oG1 + i], w = rec[a.lay.oG2 + i];
+        const float my = mt_sum(a.mtV, nbj, l, a.r4, bl, i);       // second k_bil_mt pass
+        const float mx = mt_sum(a.mtW, nbi, l, a.r4, bl, i);
+        const float c1 = hybrid ? rec[a.lay.oV1 + i] : 0.f, c2 = hybrid ? rec[a.lay.oV2 + i] : 0.f;
+        rec[a.lay.oV1 + i] = v + c1;
+        rec[a.lay.oV2 + i] = w + c2;
+        rec[a.lay.oG1 + i] = dOne * v + my + ca1 * c1;
+        rec[a.lay.oG2 + i] = mx + ca2 * c2;
+    }
 }
 
 // ---- update: 16 rows ij of the R/C tensor (viewed as (r*r, m)) against all m columns ------

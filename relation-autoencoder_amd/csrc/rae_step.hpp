@@ -6,7 +6,7 @@ namespace rae {
 
 // Per-example record in the exchange buffer (floats).
 //   P (m) | dS (m) | V1 (r) | V2 (r) | dw1 (r) | dw2 (r) | G1 (r) |
-//   [bilinear: G2 (r) | X (r) | Y (r) | A1 (r) | A2 (r) | z = S - max S (m)] |
+//   [bilinear: G2 (r) | X (r) | Y (r) | A1 (r) | A2 (r) | z = S - max S (m) | aux (4)] |
 //   coef (2*NJ) | loss (1) | pad
 // coef[j] = (c_j, gamma_j) for record j (0: e1, 1: e2, 2+t: neg1[t], 2+s+t: neg2[t]):
 // record j's A-row gradient is c_j * vec_j and its Ab gradient gamma_j, with
@@ -17,10 +17,12 @@ namespace rae {
 // bilinear : V1 = M a2 (+ wC1), V2 = M^T a1 (+ wC2) with M = sum_k P_k R[:,:,k];
 //            G1/G2 = the full A-row gradients of e1/e2; X, Y, A1, A2 the rank-2 factors of
 //            dCost/dM = X A2^T + A1 Y^T (A1/A2 = copies of A[e1], A[e2] taken before the
-//            update kernel changes A); dw1/dw2 as SP for the hybrid.
+//            update kernel changes A); dw1/dw2 as SP for the hybrid.  Forward scratch:
+//            G1/G2 hold M a2 / M^T a1 until k_bil_fin, aux = (dOne, c_a1, c_a2) from
+//            k_bil_dec.
 struct RecLayout {
     int oP, odS, oV1, oV2, odw1, odw2, oG1, ocoef, oloss, rec;
-    int oG2, oX, oY, oA1, oA2, oZ;   // bilinear decoders only (0 for SP)
+    int oG2, oX, oY, oA1, oA2, oZ, oAux;   // bilinear decoders only (0 for SP)
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
@@ -44,6 +46,7 @@ __host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s) {
         L.oA1 = o; o += r4;
         L.oA2 = o; o += r4;
         L.oZ = o; o += m4;
+        L.oAux = o; o += 4;
     }
     L.ocoef = o;
     o += align4(2 * NJ);
@@ -91,8 +94,10 @@ struct StepArgs {
     int64_t step_offset;
     float* costs;
     float* gWs;          // dense W gradient scratch (reg_on only)
-    float* Mbuf;         // bilinear: M_b = sum_k P_bk R[:,:,k] of this rank's examples (l, r*r)
     float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
+    float* mtV;          // bilinear: k_bil_mt partials over j-blocks (nblk, l, r4): M a2 / M y
+    float* mtW;          //           ... over i-blocks: M^T a1 / M^T x
+    int r4;              // align4(r): row stride of the partials
     int nib;             // bilinear: number of i-blocks of the dP contraction
     int bf16;            // bilinear: bf16 MFMA operands (fp32 accumulation) for the R GEMMs
     // bf16 R-gradient operands laid out by k_bil_prep after the exchange: the rank-2 factors

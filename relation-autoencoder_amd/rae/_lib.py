@@ -73,7 +73,7 @@ EXPORTS = (
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
-    "rae_stream_copy",
+    "rae_stream_copy", "rae_mfma_probe",
 )
 
 
@@ -152,10 +152,11 @@ def load(path: str | None = None):
     lib.rae_neg_sample_philox.argtypes = [_P, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, _P, _P]
     lib.rae_time_next.argtypes = [_P, _P, _P]
     lib.rae_stream_copy.argtypes = [_P, _P, C.c_int64, _P]
+    lib.rae_mfma_probe.argtypes = [C.c_int64, C.c_int32, _P, _P]
     lib.rae_event_create.argtypes = [C.POINTER(_P)]
     lib.rae_event_destroy.argtypes = [_P]
     lib.rae_event_elapsed_ms.argtypes = [_P, _P, C.POINTER(C.c_float)]
-    for fn in ("rae_stream_copy", "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
+    for fn in ("rae_stream_copy", "rae_mfma_probe", "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
                "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
                "rae_step_forward_at", "rae_step_update_at",

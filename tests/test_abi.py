@@ -32,9 +32,9 @@ def test_struct_layout_matches_header(built_lib):
     # 16-B aligned
     rec = built_lib.rae_exchange_record_floats(C.byref(cfg))
     assert rec == ((2 * 100 + 5 * 200 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
-    cfg.decoder = 1     # bilinear: + G2, X, Y, A1, A2 (r) + z (m)
+    cfg.decoder = 1     # bilinear: + G2, X, Y, A1, A2 (r) + z (m) + aux (4: dOne, c_a1, c_a2)
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == \
-        ((3 * 100 + 10 * 200 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
+        ((3 * 100 + 10 * 200 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
     cfg.decoder = 0
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 100
     cfg.world_size = 8

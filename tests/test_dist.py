@@ -1,10 +1,10 @@
-"""Data-parallel path with world_size 2, one process per rank, launched the way
-bench.py is launched for N > 1 (torch.distributed.run, 127.0.0.1).
+"""Data-parallel path with world_size 2 and 4, one process per rank, launched the
+way bench.py is launched for N > 1 (torch.distributed.run, 127.0.0.1).
 
 CPU (gloo): the exchange all-gather, and the row/negative-column partition + global loss
 normaliser on the float64 oracle == the single-process oracle at the global batch.
-GPU: the HIP path itself with two ranks on one GPU (gloo, host-staged exchange) == the
-oracle at the global batch, and both replicas bit-identical.
+GPU: the HIP path itself with two / four ranks on one GPU (gloo, host-staged exchange) == the
+oracle at the global batch, and all replicas bit-identical.
 """
 import os
 import socket
@@ -27,19 +27,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(args, timeout=300):
+def _launch(args, timeout=300, nproc=2):
     env = dict(os.environ)
     env["OMP_NUM_THREADS"] = "1"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, *args]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER,
+           *args]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
 
 
-def _single_process_oracle(decoder, lambda1=0.0):
+def _single_process_oracle(decoder, lambda1=0.0, ws=2):
     data, _ = _dataset()
     sp_ = data.split["train"]
-    L = 2 * DP_SHAPE["l"]
+    L = ws * DP_SHAPE["l"]
     tr = O.OracleTrainer(decoder, sp_.xFeats, sp_.args1, sp_.args2, data.negSamplingCum,
                          np.random.RandomState(2), DP_SHAPE["m"], DP_SHAPE["r"], DP_SHAPE["s"], L,
                          lr=0.1, alpha=1.0, lambda1=lambda1)
@@ -54,28 +55,29 @@ def test_exchange_all_gather_gloo(tmp_path):
         np.testing.assert_array_equal(np.load(tmp_path / f"exchange_{k}.npy"), want)
 
 
-@pytest.mark.parametrize("decoder,lambda1", [("sp", 0.0), ("rescal", 0.0), ("rescal+sp", 0.0),
-                                             ("sp", 0.01)])
-def test_partition_equals_global_batch(tmp_path, decoder, lambda1):
-    _launch(["oracle", str(tmp_path), decoder, str(lambda1)])
-    tr, costs = _single_process_oracle(decoder, lambda1)
-    r0 = np.load(tmp_path / f"oracle_{decoder}_0.npz")
-    r1 = np.load(tmp_path / f"oracle_{decoder}_1.npz")
-    np.testing.assert_allclose(r0["costs"], costs, rtol=1e-10, atol=1e-12)
+@pytest.mark.parametrize("decoder,lambda1,ws", [("sp", 0.0, 2), ("rescal", 0.0, 2),
+                                                ("rescal+sp", 0.0, 2), ("sp", 0.01, 2),
+                                                ("sp", 0.0, 4), ("rescal+sp", 0.01, 4)])
+def test_partition_equals_global_batch(tmp_path, decoder, lambda1, ws):
+    _launch(["oracle", str(tmp_path), decoder, str(lambda1)], nproc=ws)
+    tr, costs = _single_process_oracle(decoder, lambda1, ws)
+    rs = [np.load(tmp_path / f"oracle_{decoder}_{k}.npz") for k in range(ws)]
+    np.testing.assert_allclose(rs[0]["costs"], costs, rtol=1e-10, atol=1e-12)
     for k, v in tr.params.items():
-        np.testing.assert_array_equal(r0[k], r1[k])           # replicas identical
-        np.testing.assert_allclose(r0[k], v, rtol=1e-9, atol=1e-11, err_msg=k)
+        for rk in rs[1:]:
+            np.testing.assert_array_equal(rs[0][k], rk[k])    # replicas identical
+        np.testing.assert_allclose(rs[0][k], v, rtol=1e-9, atol=1e-11, err_msg=k)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder", ["sp", "rescal", "rescal+sp"])
-def test_gpu_two_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder):
-    _launch(["gpu", str(tmp_path), decoder])
-    tr, costs = _single_process_oracle(decoder)
-    g0 = np.load(tmp_path / f"gpu_{decoder}_0.npz")
-    g1 = np.load(tmp_path / f"gpu_{decoder}_1.npz")
-    np.testing.assert_allclose(g0["costs"], costs, rtol=2e-5, atol=2e-5)
+@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4)])
+def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws):
+    _launch(["gpu", str(tmp_path), decoder], nproc=ws)
+    tr, costs = _single_process_oracle(decoder, ws=ws)
+    gs = [np.load(tmp_path / f"gpu_{decoder}_{k}.npz") for k in range(ws)]
+    np.testing.assert_allclose(gs[0]["costs"], costs, rtol=2e-5, atol=2e-5)
     for k, v in tr.params.items():
-        np.testing.assert_array_equal(g0[k], g1[k])           # bit-identical replicas
-        err = np.abs(g0[k] - v)
+        for gk in gs[1:]:
+            np.testing.assert_array_equal(gs[0][k], gk[k])    # bit-identical replicas
+        err = np.abs(gs[0][k] - v)
         assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"

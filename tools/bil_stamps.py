@@ -48,21 +48,31 @@ def main():
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     lib.rae_build_index(eng.plan, 20, args.iters, st)
     per = []
+    vw = []
+    nvw = ((cfg["r"] + 7) // 8) * ((cfg["r"] + 15) // 16)
     for it in range(args.iters):
-        bf = torch.zeros(gf * 16, dtype=torch.int64, device=dev)
+        bf = torch.zeros(16384 + nvw * 8, dtype=torch.int64, device=dev)
         lib.rae_debug_stamps(eng.plan, C.c_void_p(bf.data_ptr()), 1)
         lib.rae_step_forward_at(eng.plan, 20 + it, st)
         lib.rae_debug_stamps(eng.plan, None, 1)
         lib.rae_step_update_at(eng.plan, 20 + it, st)
         torch.cuda.synchronize()
-        f = bf.cpu().numpy().reshape(gf, 16).astype(np.float64)[:, :7] / 100.0   # -> us
+        allb = bf.cpu().numpy()
+        v = allb[16384:16384 + nvw * 8].reshape(nvw, 8).astype(np.float64)[:, :6] / 100.0
+        vw.append(np.concatenate([v[:, :1] - v[:, 0].min(), np.diff(v, axis=1)], axis=1))
+        f = allb[:gf * 16].reshape(gf, 16).astype(np.float64)[:, :7] / 100.0   # -> us
         t0 = f[:, 0].min()
         per.append(np.concatenate([f[:, :1] - t0, np.diff(f, axis=1), f[:, -1:] - t0], axis=1))
     per = np.concatenate(per)
-    cols = ["start", "ids+rec", "sweep1", "negrows+dots", "coef+xy", "sweep2", "record", "end"]
+    cols = ["start", "ids+rec", "v,w+negrows", "dots", "coef+xy", "-", "record", "end"]
     print(f"k_bil_dec ({args.config}, {gf} workgroups), median/max us per phase:")
     print("  " + "  ".join(f"{c} {np.median(per[:, i]):.2f}/{per[:, i].max():.2f}"
                            for i, c in enumerate(cols)))
+    vw = np.concatenate(vw)
+    vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write"]
+    print(f"k_bil_mt pass 0 ({nvw} workgroups, wave 0 of each), median/max us per phase:")
+    print("  " + "  ".join(f"{c} {np.median(vw[:, i]):.2f}/{vw[:, i].max():.2f}"
+                           for i, c in enumerate(vcols)))
 
 
 if __name__ == "__main__":
