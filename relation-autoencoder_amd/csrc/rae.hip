@@ -81,6 +81,22 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_dp2(StepArgs a) {
     bil_gemm_dp2<NJS, MT>(a, blockIdx.x, smem);
 }
 __global__ __launch_bounds__(RAE_BT) void k_bil_prep(StepArgs a) { bil_prep(a); }
+// the R-tensor update: one wave per 16 rows (i, j) of R x all m relations (slot nCt + tile)
+__host__ __device__ inline int n_ctiles(int dec, int r, int m);
+__host__ __device__ inline int n_rtiles(int dec, int r, int m);
+template <int OPT, bool LDS>
+__global__ __launch_bounds__(RAE_BT) void k_bil_rows(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = blockIdx.x * RAE_NWAVE + w;
+    if (t >= n_rtiles(a.dec, a.r, a.m)) return;
+    const int slot = n_ctiles(a.dec, a.r, a.m) + t;
+    if constexpr (LDS)
+        task_bilinear_rows_lds<OPT>(a, t, slot, threadIdx.x & 63,
+                                    reinterpret_cast<float*>(smem) + (size_t)w * (OPT == 0 ? 2 : 1) * 16 * a.m);
+    else
+        task_bilinear_rows<OPT>(a, t, slot, threadIdx.x & 63);
+}
 __global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
     __shared__ float sdp[1024];
     __shared__ float red[2 * RAE_NWAVE];
@@ -121,12 +137,12 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 // Update launch layout (workgroups of RAE_NWAVE = 4 waves), in dispatch order:
 //   [0, nT)              one dense 16x16 tile per workgroup: C1/C2 tiles, then Wb tiles
 //                        (no row index needed: they start at once; K = batch split 4 ways)
-//   [nT, nT + nP)        one wave task each, no row index needed: the cost, R-row blocks
+//   [nT, nT + nP)        one wave task each, no row index needed: the cost
 //   then, after the batch's index header: one workgroup per very heavy A row, per very heavy
 //   W row, and the remaining workgroups' waves grid-stride over the heavy A rows, heavy W
 //   rows, light A rows, light W rows (one row per wave)
 __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
-    return 1 + n_rtiles(dec, r, m);                      // the cost + R/C row blocks
+    return 1;                                            // the cost (R rows: k_bil_rows)
 }
 #ifndef RAE_UPD_WGCAP
 #define RAE_UPD_WGCAP 1536    // row-task workgroups: 6 per CU (24 waves) on 256 CUs
@@ -158,7 +174,6 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     const int64_t ex0 = g * (int64_t)a.L;
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
     const int nCt = n_ctiles(a.dec, a.r, a.m);
-    const int nRt = n_rtiles(a.dec, a.r, a.m);
     const int nT = nCt + mt;
     const int nPt = update_wave_free_tasks(a.dec, a.r, a.m);
     const int nP = (nPt + RAE_NWAVE - 1) / RAE_NWAVE;
@@ -191,15 +206,12 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
 #endif
         return;
     }
-    if (wg < nT + nP) {                                       // cost, R-row blocks
+    if (wg < nT + nP) {                                       // the cost
         const int t = (wg - nT) * RAE_NWAVE + w;
 #ifndef RAE_SKIP_TILES
         if (t == 0) {
             RAE_FIRST(3);
             task_cost(a, lane);
-        } else if (t < nPt) {
-            RAE_FIRST(1);
-            if constexpr (BIL) task_bilinear_rows<OPT>(a, t - 1, nCt + t - 1, lane);
         }
         RAE_WAVE_END();
 #endif
@@ -768,10 +780,20 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
 template <int OPT, bool V4, bool BIL>
 static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const StepArgs& a) {
     if constexpr (BIL) {
+        // R tensor: k_bil_prep (bf16 operand layout) -> k_bil_rows; then k_update_bil (C / Wb
+        // tiles, cost, A / W rows).  Measured at C5 and not kept: a forked stream for the R
+        // branch (123 vs 112 us/step: the cross-stream graph edges cost more than the overlap);
+        // k_bil_rows with all P fragments in LDS and every load of a tile hoisted into one round
+        // trip (29 vs 24 us: two workgroups per CU and the per-workgroup staging cost more).
         if (a.bf16) {
             const int gp = 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
             RAE_LAUNCH(p, k_bil_prep, dim3(gp), bt, 0, st, a);
         }
+        const int nRt = n_rtiles(a.dec, a.r, a.m);
+        const dim3 gr((nRt + RAE_NWAVE - 1) / RAE_NWAVE);
+        const size_t lr = bil_rows_lds_bytes(a.m, a.bf16, OPT == 0);
+        if (lr) RAE_LAUNCH(p, (k_bil_rows<OPT, true>), gr, bt, lr, st, a);
+        else RAE_LAUNCH(p, (k_bil_rows<OPT, false>), gr, bt, 0, st, a);
         if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
         else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
     } else {

@@ -873,13 +873,17 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
             ua[e] = (__bf16)(ijv ? u : 0.f);
         }
 #pragma unroll
-        for (int q = 0; q < RAE_KG; ++q) {
+        for (int q = 0; q < RAE_KG; ++q) {          // D[k][ij]: P^T as A, U as B
             if (q >= nk) continue;
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, pb[q], acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb[q], ua, acc[q], 0, 0, 0);
         }
     }
 }
 
+// One wave: 16 rows ij x all m columns.  The gradient tile comes out transposed (D[k][ij]:
+// lane (li, kk) holds k = 16q + 4kk + rg of row ij = 16 ijt + li), so each lane updates four
+// consecutive parameters of one row: float4 read-modify-write, every load of the tile issued
+// before its first store (one memory round trip per column group instead of one per element).
 template <int OPT>
 __device__ void task_bilinear_rows(const StepArgs& a, int ijt, int slot, int lane) {
     const int m = a.m, r = a.r, L = a.L;
@@ -891,6 +895,7 @@ __device__ void task_bilinear_rows(const StepArgs& a, int ijt, int slot, int lan
     const int i = ijc / r, j = ijc - (ijc / r) * r;
     const int nkt = (m + 15) / 16;
     const bool reg = a.reg_on && a.ext_reg;
+    const bool vec = (m & 3) == 0;
     float l1 = 0.f, l2 = 0.f;
     for (int kg0 = 0; kg0 < nkt; kg0 += RAE_KG) {
         const int nk = min(RAE_KG, nkt - kg0);
@@ -913,30 +918,131 @@ __device__ void task_bilinear_rows(const StepArgs& a, int ijt, int slot, int lan
             }
 #pragma unroll
             for (int q = 0; q < RAE_KG; ++q)
-                if (q < nk) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, pv[q], acc[q], 0, 0, 0);
+                if (q < nk) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[q], u, acc[q], 0, 0, 0);
         }
+        auto apply = [&](float wv, float& ac, float gg) {
+            if (reg) {
+                gg += a.l1adj * sgnf(wv) + 2.f * a.l2adj * wv;
+                l1 += fabsf(wv);
+                l2 += wv * wv;
+            }
+            return opt_update<OPT>(wv, &ac, gg, a.lr);
+        };
+        if (vec) {
+            float4 wv[RAE_KG], av[RAE_KG];
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int q = 0; q < RAE_KG; ++q) {
-            if (q >= nk) continue;
-            const int k = (kg0 + q) * 16 + li;
+            for (int q = 0; q < RAE_KG; ++q) {
+                const int k0 = (kg0 + q) * 16 + 4 * kk;
+                const bool ok = q < nk && ijv && k0 < m;
+                const int64_t o = ok ? ij * m + k0 : 0;
+                wv[q] = ok ? *reinterpret_cast<const float4*>(a.R3 + o) : z4;
+                av[q] = (OPT == 0 && ok) ? *reinterpret_cast<const float4*>(a.aR3 + o) : z4;
+            }
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) {
-                const int64_t row = (int64_t)ijt * 16 + kk * 4 + rg;
-                if (row < rr && k < m) {
-                    const int64_t o = row * m + k;
-                    const float wv = a.R3[o];
-                    float gg = acc[q][rg];
-                    if (reg) {
-                        gg += a.l1adj * sgnf(wv) + 2.f * a.l2adj * wv;
-                        l1 += fabsf(wv);
-                        l2 += wv * wv;
-                    }
+            for (int q = 0; q < RAE_KG; ++q) {
+                const int k0 = (kg0 + q) * 16 + 4 * kk;
+                if (!(q < nk && ijv && k0 < m)) continue;
+                const int64_t o = ij * m + k0;
+                float4 w = wv[q], ac = av[q];
+                w.x = apply(w.x, ac.x, acc[q][0]);
+                w.y = apply(w.y, ac.y, acc[q][1]);
+                w.z = apply(w.z, ac.z, acc[q][2]);
+                w.w = apply(w.w, ac.w, acc[q][3]);
+                *reinterpret_cast<float4*>(a.R3 + o) = w;
+                if (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + o) = ac;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < RAE_KG; ++q) {
+                if (q >= nk || !ijv) continue;
+#pragma unroll
+                for (int rg = 0; rg < 4; ++rg) {
+                    const int k = (kg0 + q) * 16 + 4 * kk + rg;
+                    if (k >= m) continue;
+                    const int64_t o = ij * m + k;
                     float ac = (OPT == 0) ? a.aR3[o] : 0.f;
-                    a.R3[o] = opt_update<OPT>(wv, &ac, gg, a.lr);
+                    a.R3[o] = apply(a.R3[o], ac, acc[q][rg]);
                     if (OPT == 0) a.aR3[o] = ac;
                 }
             }
         }
+    }
+    if (reg) {
+        const double L1 = wave_sum_d((double)l1), L2 = wave_sum_d((double)l2);
+        if (lane == 0) {
+            a.regpart[2 * slot] = L1;
+            a.regpart[2 * slot + 1] = L2;
+        }
+    }
+}
+
+// k_bil_rows' fast path (bf16 operands, m % 4 == 0, m <= RAE_RT_LDS_M): the wave's 16 rows
+// of R and of the optimizer state are one contiguous 64m-byte run each; they are copied into
+// the wave's LDS slice by direct global->LDS loads (global_load_lds_dwordx4: lane-linear
+// 1 KB per instruction) issued BEFORE the gradient, so the parameter reads are in flight
+// during it -- all waves of the launch start together, and with loads after the gradient
+// the latency-bound gradient phase and the HBM-bound read-modify-write phase never overlap
+// (measured at C5: 8.2 + 16.7 us sequential).  Then float4 read-modify-write from LDS,
+// float4 stores to HBM.
+#define RAE_RT_LDS_M 128
+__host__ __device__ inline size_t bil_rows_lds_bytes(int m, bool bf16, bool adagrad) {
+    return (bf16 && (m & 3) == 0 && m <= RAE_RT_LDS_M) ? (size_t)RAE_NWAVE * (adagrad ? 2 : 1) * 16 * m * 4 : 0;
+}
+template <int OPT>
+__device__ void task_bilinear_rows_lds(const StepArgs& a, int ijt, int slot, int lane, float* sw) {
+    typedef __attribute__((address_space(3))) void lds_void_t;
+    typedef __attribute__((address_space(1))) void glb_void_t;
+    const int m = a.m, r = a.r;
+    const int64_t rr = (int64_t)r * r;
+    const int li = lane & 15, kk = lane >> 4;
+    const int64_t ij = (int64_t)ijt * 16 + li;
+    const bool ijv = ij < rr;
+    const int64_t base = (int64_t)ijt * 16 * m;
+    const int nrow = (int)min((int64_t)16, rr - (int64_t)ijt * 16);
+    const int nv = nrow * m / 4;                          // float4s of the tile
+    float* sR = sw;
+    float* sA = sw + 16 * m;
+    for (int n = 0; n * 64 < nv; ++n) {
+        const int idx = n * 64 + lane;
+        if (idx < nv) {
+            __builtin_amdgcn_global_load_lds((glb_void_t*)(a.R3 + base + 4 * idx),
+                                             (lds_void_t*)(sR + n * 256), 16, 0, 0);
+            if constexpr (OPT == 0)
+                __builtin_amdgcn_global_load_lds((glb_void_t*)(a.aR3 + base + 4 * idx),
+                                                 (lds_void_t*)(sA + n * 256), 16, 0, 0);
+        }
+    }
+    const bool reg = a.reg_on && a.ext_reg;
+    float l1 = 0.f, l2 = 0.f;
+    rae_bf4 acc[RAE_KG];
+#pragma unroll
+    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+    const int nk = (m + 15) / 16;                         // <= RAE_KG: one column group
+    bilinear_rows_acc_bf16(a, ijt, 0, nk, acc, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the tile has landed in LDS
+#pragma unroll
+    for (int q = 0; q < RAE_KG; ++q) {
+        const int k0 = q * 16 + 4 * kk;
+        if (!(q < nk && ijv && k0 < m)) continue;
+        const int lo = li * m + k0;
+        float4 w = *reinterpret_cast<const float4*>(sR + lo);
+        float4 ac = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (OPT == 0) ac = *reinterpret_cast<const float4*>(sA + lo);
+        float* wp = &w.x;
+        float* ap = &ac.x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float gg = acc[q][e];
+            if (reg) {
+                gg += a.l1adj * sgnf(wp[e]) + 2.f * a.l2adj * wp[e];
+                l1 += fabsf(wp[e]);
+                l2 += wp[e] * wp[e];
+            }
+            wp[e] = opt_update<OPT>(wp[e], &ap[e], gg, a.lr);
+        }
+        *reinterpret_cast<float4*>(a.R3 + base + lo) = w;
+        if constexpr (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + base + lo) = ac;
     }
     if (reg) {
         const double L1 = wave_sum_d((double)l1), L2 = wave_sum_d((double)l2);
