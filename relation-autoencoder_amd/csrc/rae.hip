@@ -76,7 +76,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_dp(StepArgs a) {
     else bil_gemm_dp(a, t, threadIdx.x & 63);
 }
 template <int NJS, int MT>
-__global__ __launch_bounds__(RAE_BT) void k_bil_dp2(StepArgs a) {
+__global__ __launch_bounds__((dp2_threads<NJS, MT>())) void k_bil_dp2(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_gemm_dp2<NJS, MT>(a, blockIdx.x, smem);
 }
@@ -97,10 +97,11 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_rows(StepArgs a) {
     else
         task_bilinear_rows<OPT>(a, t, slot, threadIdx.x & 63);
 }
-__global__ __launch_bounds__(RAE_BT) void k_bil_fin(StepArgs a) {
-    __shared__ float sdp[1024];
-    __shared__ float red[2 * RAE_NWAVE];
-    bil_finish(a, blockIdx.x, sdp, red);
+__global__ __launch_bounds__(RAE_FINT) void k_bil_fin(StepArgs a) {
+    __shared__ float sdp[1024];          // NS * m <= max(RAE_FINT, m) <= 1024
+    __shared__ float smt[4 * 1024];      // M-tile half sums, r <= 1024
+    __shared__ float red[2 * RAE_FINW];
+    bil_finish(a, blockIdx.x, sdp, smt, red);
 }
 
 // shapes with compile-time specialisations of the forward kernel (BASELINE.json configs
@@ -753,14 +754,14 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
     const size_t lds77 = dp2_lds_bytes<7, 7>(), lds88 = dp2_lds_bytes<8, 8>();
     if (p->dp2 == 1)
-        RAE_LAUNCH(p, (k_bil_dp2<7, 7>), dim3(a.nib), dim3(RAE_BT), lds77, st, a);
+        RAE_LAUNCH(p, (k_bil_dp2<7, 7>), dim3(a.nib), dim3(dp2_threads<7, 7>()), lds77, st, a);
     else if (p->dp2 == 2)
-        RAE_LAUNCH(p, (k_bil_dp2<8, 8>), dim3(a.nib), dim3(RAE_BT), lds88, st, a);
+        RAE_LAUNCH(p, (k_bil_dp2<8, 8>), dim3(a.nib), dim3(dp2_threads<8, 8>()), lds88, st, a);
     else if (a.bf16)
         RAE_LAUNCH(p, k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
     else
         RAE_LAUNCH(p, k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
-    RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_BT), 0, st, a);
+    RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_FINT), 0, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {

@@ -275,21 +275,38 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     }
 }
 
-// sum of the per-block partials of one example's M-tile output (four interleaved chains, a
-// fixed order: the loads are independent)
-__device__ __forceinline__ float mt_sum(const float* part, int nblk, int l, int r4, int b, int i) {
+// sum of the per-block partials [q0, q1) of one example's M-tile output (four interleaved
+// chains, a fixed order: the loads are independent)
+__device__ __forceinline__ float mt_sum(const float* part, int q0, int q1, int l, int r4, int b, int i) {
     const float* p = part + (int64_t)b * r4 + i;
     const int64_t st = (int64_t)l * r4;
     float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-    int q = 0;
-    for (; q + 4 <= nblk; q += 4) {
+    int q = q0;
+    for (; q + 4 <= q1; q += 4) {
         t0 += p[q * st];
         t1 += p[(q + 1) * st];
         t2 += p[(q + 2) * st];
         t3 += p[(q + 3) * st];
     }
-    for (; q < nblk; ++q) t0 += p[q * st];
+    for (; q < q1; ++q) t0 += p[q * st];
     return (t0 + t1) + (t2 + t3);
+}
+// One example's M-tile sums with four threads per element i: quarter qd of the workgroup's
+// index space sums half the partials of one output -- qd 0/1: the j-block partials (mtV),
+// qd 2/3: the i-block partials (mtW) -- into q0v / q1v / q0w / q1w; the caller combines the
+// halves in order (after a barrier).
+template <int T>
+__device__ __forceinline__ void mt_sums_split(const StepArgs& a, int b, float* q0v, float* q1v,
+                                              float* q0w, float* q1w) {
+    const int r = a.r, r4 = a.r4;
+    const int nbi = (r + RAE_MTI - 1) / RAE_MTI, nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
+    for (int e = threadIdx.x; e < 4 * r4; e += T) {
+        const int qd = e / r4, i = e - qd * r4;
+        const int n = qd < 2 ? nbj : nbi, h = n / 2;
+        const float t = i < r ? mt_sum(qd < 2 ? a.mtV : a.mtW, (qd & 1) ? h : 0, (qd & 1) ? n : h,
+                                       a.l, r4, b, i) : 0.f;
+        (qd == 0 ? q0v : qd == 1 ? q1v : qd == 2 ? q0w : q1w)[i] = t;
+    }
 }
 
 // dP partials (as bil_gemm_dp) with bf16 operands; K = j in steps of 32
@@ -358,10 +375,15 @@ __device__ void bil_gemm_dp_bf16(const StepArgs& a, int t, int lane) {
 // in block order by bil_finish (deterministic).  Shapes: r <= 32 NJS, m <= 16 MT,
 // r % 4 == m % 4 == 0.
 #define RAE_IB2 2    // i rows per k_bil_dp2 workgroup (the q-loop selects x/a1 for q < 2)
+// threads per k_bil_dp2 workgroup: 512 for C5's <7, 7> (its 7 example tiles in one round);
+// <8, 8> needs more than the 256 VGPRs an 8-wave workgroup allows, so it keeps 4 waves
+template <int NJS, int MT>
+constexpr int dp2_threads() { return (NJS >= 8 || MT >= 8) ? 256 : 512; }
 template <int NJS, int MT>
 constexpr size_t dp2_lds_bytes() { return (size_t)RAE_IB2 * MT * 16 * (NJS * 32 + 8) * 2; }
 template <int NJS, int MT>
 __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
+    constexpr int RAE_DP2T = dp2_threads<NJS, MT>();
     // LDS row stride JS = JP + 8 bf16: 16-B aligned fragment reads, and the 16 rows k a
     // fragment read touches land on distinct bank groups
     constexpr int JP = NJS * 32, KP = MT * 16, JS = JP + 8;
@@ -373,21 +395,21 @@ __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
     const int ni = min(RAE_IB2, r - i0);
     // stage: R[i0+q][j][k] -> lds[q][k][j] (bf16, round to nearest even); the padding
     // (j >= r, k >= m) is zero.
-    for (int e = tid; e < RAE_IB2 * KP * JS / 8; e += RAE_BT)
+    for (int e = tid; e < RAE_IB2 * KP * JS / 8; e += RAE_DP2T)
         reinterpret_cast<uint4*>(lds)[e] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     // A staging unit is 8 rows j x one float4 of k: its 8 loads are lanes' consecutive
     // 16-B chunks of whole rows (coalesced), and its 4 LDS stores are 16-B runs of 8 j at
     // one k (ds_write_b128).  All of a slice's loads are issued before its first store.
     const int m4 = m / 4, r8 = (r + 7) / 8, nunit = r8 * m4;
-    constexpr int UU = ((JP / 8) * (KP / 4) + RAE_BT - 1) / RAE_BT;
+    constexpr int UU = ((JP / 8) * (KP / 4) + RAE_DP2T - 1) / RAE_DP2T;
     for (int q = 0; q < ni; ++q) {
         const float4* src = reinterpret_cast<const float4*>(a.R3 + (int64_t)(i0 + q) * r * m);
         __bf16* dst = lds + q * KP * JS;
         float4 v[UU][8];
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
-            const int e = tid + u * RAE_BT;
+            const int e = tid + u * RAE_DP2T;
             const bool ok = e < nunit;
             const int jb = ok ? e / m4 : 0, kq = ok ? e - jb * m4 : 0;
 #pragma unroll
@@ -399,7 +421,7 @@ __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
         }
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
-            const int e = tid + u * RAE_BT;
+            const int e = tid + u * RAE_DP2T;
             if (e < nunit) {
                 const int jb = e / m4, kq = e - jb * m4;
                 __bf16* d = dst + 4 * kq * JS + 8 * jb;
@@ -420,7 +442,7 @@ __device__ void bil_gemm_dp2(const StepArgs& a, int ib, char* smem) {
     }
     __syncthreads();
     const int nbt = (l + 15) / 16;
-    for (int bt = w; bt < nbt; bt += RAE_NWAVE) {
+    for (int bt = w; bt < nbt; bt += RAE_DP2T / RAE_WAVE) {
         const int b = bt * 16 + li;
         const bool bv = b < l;
         const float* er = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec;
@@ -573,18 +595,15 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         const VT* src = reinterpret_cast<const VT*>(a.A + (int64_t)S.ids[2 + t] * r);
         reinterpret_cast<VT*>(S.rows)[t * r4v + c] = src[c];
     }
-    {
-        const int nbi = (r + RAE_MTI - 1) / RAE_MTI, nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
-        for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
-            const bool iv = i < r;
-            const float v = iv ? mt_sum(a.mtV, nbj, a.l, a.r4, bl, i) : 0.f;
-            const float w = iv ? mt_sum(a.mtW, nbi, a.l, a.r4, bl, i) : 0.f;
-            S.v[i] = v;
-            S.w[i] = w;
-            if (iv) {
-                rec[a.lay.oG1 + i] = v;                   // for k_bil_fin
-                rec[a.lay.oG2 + i] = w;
-            }
+    mt_sums_split<RAE_DBT>(a, bl, S.v, S.My, S.w, S.Mtx);    // My / Mtx: scratch halves here
+    __syncthreads();
+    for (int i = threadIdx.x; i < r4; i += RAE_DBT) {
+        const float v = S.v[i] + S.My[i], w = S.w[i] + S.Mtx[i];
+        S.v[i] = v;
+        S.w[i] = w;
+        if (i < r) {
+            rec[a.lay.oG1 + i] = v;                       // for k_bil_fin
+            rec[a.lay.oG2 + i] = w;
         }
     }
     __syncthreads();
@@ -740,17 +759,37 @@ __device__ void bil_gemm_dp(const StepArgs& a, int t, int lane) {
 }
 
 // ---- k_bil_fin: dP -> dS -------------------------------------------------------------------
-__device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
+// RAE_FINT threads (16 waves): the dP partial sums are split NS = RAE_FINT / m ways (each
+// split sums every NS-th i-block partial in order; the splits are combined in order), so a
+// thread has ~nib / NS independent loads instead of nib.
+#define RAE_FINT 1024
+#define RAE_FINW (RAE_FINT / RAE_WAVE)
+__device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, float* red) {
     const int m = a.m, r = a.r, l = a.l;
     const bool hybrid = a.dec == 2;
     const int bg = a.rank * l + bl;
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     const float ce = 2.f * a.alpha * a.invD;      // entropy term, centred form (softmax_backward)
+    const int NS = max(1, RAE_FINT / m);
+    for (int e = threadIdx.x; e < NS * m; e += RAE_FINT) {
+        const int sp = e / m, k = e - sp * m;
+        const float* pp = a.dPpart + (int64_t)bl * m + k;
+        const int64_t st = (int64_t)l * m;
+        float t0 = 0.f, t1 = 0.f;
+        int ib = sp;
+        for (; ib + NS < a.nib; ib += 2 * NS) {
+            t0 += pp[ib * st];
+            t1 += pp[(ib + NS) * st];
+        }
+        if (ib < a.nib) t0 += pp[ib * st];
+        sdp[e] = t0 + t1;
+    }
+    mt_sums_split<RAE_FINT>(a, bl, smt, smt + 1024, smt + 2048, smt + 3072);
+    __syncthreads();
     float sd = 0.f, sz = 0.f;
-    for (int k = threadIdx.x; k < m; k += RAE_BT) {
+    for (int k = threadIdx.x; k < m; k += RAE_FINT) {
         float dp = 0.f;
-#pragma unroll 10
-        for (int ib = 0; ib < a.nib; ++ib) dp += a.dPpart[((int64_t)ib * l + bl) * m + k];
+        for (int sp = 0; sp < NS; ++sp) dp += sdp[sp * m + k];
         if (hybrid) {
             float h = 0.f;
             for (int i = 0; i < r; ++i)
@@ -758,24 +797,23 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* red) {
                      rec[a.lay.odw2 + i] * a.C2[(int64_t)i * m + k];
             dp += h;
         }
-        sdp[k] = dp;
         const float p = rec[a.lay.oP + k];
         sd += p * dp;
         sz += p * rec[a.lay.oZ + k];
+        rec[a.lay.odS + k] = dp;                      // dP, scaled below
     }
-    sd = block_sum<RAE_BT>(sd, red);
-    sz = block_sum<RAE_BT>(sz, red + RAE_NWAVE);
-    for (int k = threadIdx.x; k < m; k += RAE_BT)
-        rec[a.lay.odS + k] = rec[a.lay.oP + k] * ((sdp[k] - sd) + ce * (rec[a.lay.oZ + k] - sz));
+    sd = block_sum<RAE_FINT>(sd, red);
+    sz = block_sum<RAE_FINT>(sz, red + RAE_FINW);
+    for (int k = threadIdx.x; k < m; k += RAE_FINT)
+        rec[a.lay.odS + k] = rec[a.lay.oP + k] * ((rec[a.lay.odS + k] - sd) + ce * (rec[a.lay.oZ + k] - sz));
     // the A-row gradient vectors (rae_step.hpp), from v = M a2, w = M^T a1 (record G1 / G2),
     // M y, M^T x (My / MtX) and the hybrid's wC1 / wC2 (V1 / V2):
     //   V1 = v + wC1,  V2 = w + wC2,  G1 = dOne v + M y + c_a1 wC1,  G2 = M^T x + c_a2 wC2
     const float dOne = rec[a.lay.oAux + 0], ca1 = rec[a.lay.oAux + 1], ca2 = rec[a.lay.oAux + 2];
-    const int nbi = (r + RAE_MTI - 1) / RAE_MTI, nbj = (r + RAE_MTJ - 1) / RAE_MTJ;
-    for (int i = threadIdx.x; i < r; i += RAE_BT) {
+    for (int i = threadIdx.x; i < r; i += RAE_FINT) {
         const float v = rec[a.lay.oG1 + i], w = rec[a.lay.oG2 + i];
-        const float my = mt_sum(a.mtV, nbj, l, a.r4, bl, i);       // second k_bil_mt pass
-        const float mx = mt_sum(a.mtW, nbi, l, a.r4, bl, i);
+        const float my = smt[i] + smt[1024 + i];                   // second k_bil_mt pass
+        const float mx = smt[2048 + i] + smt[3072 + i];
         const float c1 = hybrid ? rec[a.lay.oV1 + i] : 0.f, c2 = hybrid ? rec[a.lay.oV2 + i] : 0.f;
         rec[a.lay.oV1 + i] = v + c1;
         rec[a.lay.oV2 + i] = w + c2;
