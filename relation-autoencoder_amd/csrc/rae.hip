@@ -22,6 +22,7 @@
 
 #include "../../include/rae.h"
 #include "rae_bilinear.hpp"
+#include "rae_sp_split.hpp"
 #include "rae_common.hpp"
 #include "rae_index.hpp"
 #include "rae_label.hpp"
@@ -47,6 +48,30 @@ void k_forward(StepArgs a) {
     const int64_t g = step_batch(a);
     if constexpr (D::fixed && V4) sp_example_fast<D>(a, g, blockIdx.x, smem);
     else sp_example<V4, D>(a, g, blockIdx.x, smem);
+}
+
+// ---- split SP forward for large runtime shapes (rae_sp_split.hpp) ----
+template <bool V4>
+__global__ __launch_bounds__(RAE_FBT) void k_sp_enc(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    sp_split_enc<V4>(a, step_batch(a), blockIdx.x, smem);
+}
+__global__ __launch_bounds__(RAE_BT) void k_sp_cp(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
+    sp_split_cp(a, blockIdx.x, red);
+}
+template <bool V4>
+__global__ __launch_bounds__(RAE_FBT) void k_sp_dec(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    sp_split_dec<V4>(a, step_batch(a), blockIdx.x, smem);
+}
+__global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
+    sp_split_ctdw(a, blockIdx.x, red);
+}
+__global__ __launch_bounds__(RAE_BT) void k_sp_fin(StepArgs a) {
+    __shared__ float red[2 * RAE_NWAVE];
+    sp_split_fin(a, blockIdx.x, red);
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
@@ -145,6 +170,9 @@ __host__ __device__ inline int n_rtiles(int dec, int r, int m) {
 __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
     return 1;                                            // the cost (R rows: k_bil_rows)
 }
+#ifndef RAE_SPLIT_RM
+#define RAE_SPLIT_RM 32768    // r*m above which the SP forward runs split (rae_sp_split.hpp)
+#endif
 #ifndef RAE_UPD_WGCAP
 #define RAE_UPD_WGCAP 1536    // row-task workgroups: 6 per CU (24 waves) on 256 CUs
 #endif
@@ -412,7 +440,9 @@ struct rae_plan {
     size_t smem_fwd = 0;
     size_t smem_idx = 0;
     size_t smem_dec = 0;
-    size_t smem_mt = 0;     // k_bil_mt: one 16 x 16 x m block of R in LDS
+    size_t smem_mt = 0;     // k_bil_mt: one 8 x 16 x m block of R in LDS
+    bool sp_split = false;  // SP forward as enc -> GEMM -> dec -> GEMM -> fin (large shapes)
+    size_t smem_spe = 0;    // k_sp_enc
     bool mt_bf16 = false;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
@@ -609,6 +639,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const int64_t nbi_mt = (c.embed + RAE_MTI - 1) / RAE_MTI, nbj_mt = (c.embed + RAE_MTJ - 1) / RAE_MTJ;
     const size_t o_mtv = bil ? take(4ull * nbj_mt * c.batch_size * a.r4) : 0;
     const size_t o_mtw = bil ? take(4ull * nbi_mt * c.batch_size * a.r4) : 0;
+    // split SP forward (rae_sp_split.hpp) for runtime shapes whose decoder matrices stream
+    // through every example's workgroup (r*m > RAE_SPLIT_RM; C4: 90 k); RAE_SPSPLIT=0/1 forces
+    const char* splitenv = getenv("RAE_SPSPLIT");
+    p->sp_split = !bil && (int64_t)c.embed * c.relations > RAE_SPLIT_RM;
+    if (splitenv && (splitenv[0] == '0' || splitenv[0] == '1')) p->sp_split = !bil && splitenv[0] == '1';
+    const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
     a.Lp = (L + 31) / 32 * 32;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
@@ -636,6 +672,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
     a.dPpart = bil ? reinterpret_cast<float*>(p->ws + o_dpp) : nullptr;
+    a.dPs = p->sp_split ? reinterpret_cast<float*>(p->ws + o_dps) : nullptr;
     a.mtV = bil ? reinterpret_cast<float*>(p->ws + o_mtv) : nullptr;
     a.mtW = bil ? reinterpret_cast<float*>(p->ws + o_mtw) : nullptr;
     a.facT = a.bf16 ? reinterpret_cast<float*>(p->ws + o_fac) : nullptr;
@@ -647,6 +684,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t smem_ex = 4ull * ex_floats;
     p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP;
     p->smem_fwd = smem_ex;
+    p->smem_spe = p->sp_split ? 4ull * example_smem_floats(0, c.relations, c.embed, 0) : 0;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
     // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
     p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
@@ -670,10 +708,17 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                              (const void*)k_forward<false, DimsC2>,
                              (const void*)k_forward<true, DynDims>,
                              (const void*)k_forward<false, DynDims>,
-                             (const void*)k_bil_enc<true>, (const void*)k_bil_enc<false>};
+                             (const void*)k_bil_enc<true>, (const void*)k_bil_enc<false>,
+                             (const void*)k_sp_dec<true>, (const void*)k_sp_dec<false>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p->smem_fwd);
+        if (p->sp_split) {
+            (void)hipFuncSetAttribute((const void*)k_sp_enc<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_spe);
+            (void)hipFuncSetAttribute((const void*)k_sp_enc<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_spe);
+        }
         if (bil) {
             (void)hipFuncSetAttribute((const void*)k_bil_dp2<7, 7>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<7, 7>());
@@ -729,6 +774,17 @@ extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t strea
 
 static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 gr(p->grid_fwd), bt(RAE_FBT);
+    if (p->sp_split) {
+        const dim3 gcp(sp_cp_tasks(a.l, a.r)), gct(sp_ctdw_tasks(a.l, a.m));   // WG per tile
+        if (p->v4) RAE_LAUNCH(p, k_sp_enc<true>, gr, bt, p->smem_spe, st, a);
+        else RAE_LAUNCH(p, k_sp_enc<false>, gr, bt, p->smem_spe, st, a);
+        RAE_LAUNCH(p, k_sp_cp, gcp, dim3(RAE_BT), 0, st, a);
+        if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gr, bt, p->smem_fwd, st, a);
+        else RAE_LAUNCH(p, k_sp_dec<false>, gr, bt, p->smem_fwd, st, a);
+        RAE_LAUNCH(p, k_sp_ctdw, gct, dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_sp_fin, gr, dim3(RAE_BT), 0, st, a);
+        return;
+    }
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;
     const bool c2 = a.m == 30 && a.r == 100 && a.s == 10;
     if (c3 && p->v4)

@@ -492,6 +492,80 @@ __device__ __forceinline__ void sp_weighted_rows(const D& Dm, ExampleSmem& S) {
     }
 }
 
+// dot products of the example's A rows with wC1 / wC2 (S.srows, S.swC1, S.swC2 -> S.sdots):
+// row rho on wave rho % NW; lanes over vector columns
+template <bool V4, class D>
+__device__ __forceinline__ void sp_dots(const D& Dm, ExampleSmem& S) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int r = Dm.r, s = Dm.s, NR = 1 + 2 * s, r4 = align4(r);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    {
+        const int rv = r / VW, r4v = r4 / VW;
+        const VT* Rv = reinterpret_cast<const VT*>(S.srows);
+        const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
+        const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
+        for (int rho = w; rho < NR; rho += RAE_FNW) {
+            const VT* wv = rho > s ? W2 : W1;      // rows 1..s: neg1, s+1..2s: neg2
+            float d1 = 0.f, d2 = 0.f;
+            for (int c = lane; c < rv; c += RAE_WAVE) {
+                const VT x = Rv[rho * r4v + c];
+                d1 += vdot(x, wv[c]);
+                if (rho == 0) d2 += vdot(x, W2[c]);
+            }
+            d1 = wave_sum(d1);
+            if (rho == 0) d2 = wave_sum(d2);
+            if (lane == 0) {
+                if (rho == 0) {
+                    S.sdots[0] = d1;     // left  = <wC1, A[e1]>
+                    S.sdots[1] = d2;     // right = <wC2, A[e1]>
+                } else {
+                    S.sdots[rho + 1] = d1;   // record j = rho + 1
+                }
+            }
+        }
+    }
+}
+
+// scores, loss, coefficients (wave 0): S.sdots, S.sAbv, H -> S.scoef, loss in S.sred[32]
+template <class D>
+__device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                                float H) {
+    const int s = Dm.s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w == 0) {
+        const float left = S.sdots[0], right = S.sdots[1];
+        float sdg1 = 0.f, sdg2 = 0.f, sls = 0.f;
+        for (int t = lane; t < s; t += RAE_WAVE) {
+            const float g1 = S.sdots[2 + t] + right + S.sAbv[2 + t];
+            const float g2 = S.sdots[2 + s + t] + left + S.sAbv[2 + s + t];
+            const float dg1 = sigmoid(g1) * a.invD;
+            const float dg2 = sigmoid(g2) * a.invD;
+            float* c1 = S.scoef + 3 * (2 + t);
+            float* c2 = S.scoef + 3 * (2 + s + t);
+            c1[0] = dg1; c1[1] = 0.f; c1[2] = dg1;
+            c2[0] = 0.f; c2[1] = dg2; c2[2] = dg2;
+            sdg1 += dg1;
+            sdg2 += dg2;
+            sls += log_sigmoid(-g1) + log_sigmoid(-g2);
+        }
+        sdg1 = wave_sum(sdg1);
+        sdg2 = wave_sum(sdg2);
+        sls = wave_sum(sls);
+        if (lane == 0) {
+            const float one = left + right;
+            const float u1 = one + S.sAbv[0], u2 = one + S.sAbv[1];
+            const float du1 = -sigmoid(-u1) * a.invD;
+            const float du2 = -sigmoid(-u2) * a.invD;
+            const float dl = du1 + du2 + sdg2;     // d cost / d left
+            const float dr = du1 + du2 + sdg1;     // d cost / d right
+            S.scoef[0] = dl; S.scoef[1] = dr; S.scoef[2] = du1;
+            S.scoef[3] = 0.f; S.scoef[4] = 0.f; S.scoef[5] = du2;
+            S.sred[32] = log_sigmoid(u1) + log_sigmoid(u2) + 2.f * H + sls;
+        }
+    }
+}
+
 // ---- the SP example path ---------------------------------------------------------------
 template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
@@ -531,32 +605,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     __syncthreads();
     RAE_STAMP(a, 3);
 
-    // dot products: row rho on wave rho % NW; lanes over vector columns
-    {
-        const int rv = r / VW, r4v = r4 / VW;
-        const VT* Rv = reinterpret_cast<const VT*>(S.srows);
-        const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
-        const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
-        for (int rho = w; rho < NR; rho += RAE_FNW) {
-            const VT* wv = rho > s ? W2 : W1;      // rows 1..s: neg1, s+1..2s: neg2
-            float d1 = 0.f, d2 = 0.f;
-            for (int c = lane; c < rv; c += RAE_WAVE) {
-                const VT x = Rv[rho * r4v + c];
-                d1 += vdot(x, wv[c]);
-                if (rho == 0) d2 += vdot(x, W2[c]);
-            }
-            d1 = wave_sum(d1);
-            if (rho == 0) d2 = wave_sum(d2);
-            if (lane == 0) {
-                if (rho == 0) {
-                    S.sdots[0] = d1;     // left  = <wC1, A[e1]>
-                    S.sdots[1] = d2;     // right = <wC2, A[e1]>
-                } else {
-                    S.sdots[rho + 1] = d1;   // record j = rho + 1
-                }
-            }
-        }
-    }
+    sp_dots<V4>(Dm, S);
     __syncthreads();
     RAE_STAMP(a, 4);
 
@@ -566,37 +615,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     for (int rep = 0; rep < 2; ++rep) {
     if (rep == 1) RAE_STAMP(a, 10);
 #endif
-    if (w == 0) {
-        const float left = S.sdots[0], right = S.sdots[1];
-        float sdg1 = 0.f, sdg2 = 0.f, sls = 0.f;
-        for (int t = lane; t < s; t += RAE_WAVE) {
-            const float g1 = S.sdots[2 + t] + right + S.sAbv[2 + t];
-            const float g2 = S.sdots[2 + s + t] + left + S.sAbv[2 + s + t];
-            const float dg1 = sigmoid(g1) * a.invD;
-            const float dg2 = sigmoid(g2) * a.invD;
-            float* c1 = S.scoef + 3 * (2 + t);
-            float* c2 = S.scoef + 3 * (2 + s + t);
-            c1[0] = dg1; c1[1] = 0.f; c1[2] = dg1;
-            c2[0] = 0.f; c2[1] = dg2; c2[2] = dg2;
-            sdg1 += dg1;
-            sdg2 += dg2;
-            sls += log_sigmoid(-g1) + log_sigmoid(-g2);
-        }
-        sdg1 = wave_sum(sdg1);
-        sdg2 = wave_sum(sdg2);
-        sls = wave_sum(sls);
-        if (lane == 0) {
-            const float one = left + right;
-            const float u1 = one + S.sAbv[0], u2 = one + S.sAbv[1];
-            const float du1 = -sigmoid(-u1) * a.invD;
-            const float du2 = -sigmoid(-u2) * a.invD;
-            const float dl = du1 + du2 + sdg2;     // d cost / d left
-            const float dr = du1 + du2 + sdg1;     // d cost / d right
-            S.scoef[0] = dl; S.scoef[1] = dr; S.scoef[2] = du1;
-            S.scoef[3] = 0.f; S.scoef[4] = 0.f; S.scoef[5] = du2;
-            S.sred[32] = log_sigmoid(u1) + log_sigmoid(u2) + 2.f * H + sls;
-        }
-    }
+    sp_coefficients(a, Dm, S, H);
     __syncthreads();
 #ifdef RAE_ICACHE_TEST
     if (rep == 1) RAE_STAMP(a, 11);

@@ -1,0 +1,232 @@
+// Split SP forward for large runtime shapes (C4: r x m = 90 k floats per decoder matrix).
+//
+// The fused example kernel (rae_sp.hpp sp_example) streams C1 and C2 through every example's
+// workgroup twice (C.P, then C^T.dw): 1.4 MB per example at C4, so the forward is bound by
+// each CU's fill rate from L2.  Here the two matrix products run once for the rank's whole
+// batch as fp32-MFMA GEMMs, and the per-example work is split around them:
+//   k_sp_enc   per example : S = X.W + Wb, P = softmax(S), H          -> record P; z, H parked
+//   k_sp_cp    GEMM        : V1 = P C1^T, V2 = P C2^T  (l x r, K = m)  -> record V1, V2
+//   k_sp_dec   per example : A rows, dots, scores, loss, coefficients, dw1, dw2, G1
+//   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r) -> workspace dPs
+//   k_sp_fin   per example : centred softmax backward                  -> record dS
+// Same arithmetic as sp_example (SelectionalPreferences.py:30-51, RelationClassifier.py:35-36,
+// OieModel.py:81); only the fp32 summation order of the two products differs.  Until k_sp_fin
+// the record's dS slot holds z = S - max S and, until k_sp_dec, its loss slot holds H.
+#pragma once
+#include "rae_sp.hpp"
+
+namespace rae {
+
+typedef float rae_f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool V4>
+__device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
+    const DynDims Dm(a);
+    const int m = Dm.m;
+    ExampleSmem S = carve_example_smem(smem, 0, m, Dm.r, 0);      // no A rows here
+    const int bg = a.rank * a.l + bl;
+    const int64_t ex = g * (int64_t)a.L + bg;
+    if (threadIdx.x == 0) {
+        S.sint[0] = a.indptr[ex];
+        S.sint[1] = a.indptr[ex + 1];
+    }
+    __syncthreads();
+    CCache<V4, DynDims> cc_;                                       // unused: no C here
+    encoder_forward<V4, V4, false>(a, Dm, S, 0, 1, cc_);
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    for (int k = threadIdx.x; k < m; k += RAE_FBT) {
+        rec[a.lay.oP + k] = S.sP[k];
+        rec[a.lay.odS + k] = S.sZ[k];
+    }
+    if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];
+}
+
+// four fp32 MFMAs over a 16-deep K chunk: lane (li, g) supplies K = k0 + 4g + j for MFMA j
+__device__ __forceinline__ rae_f32x4 mfma4_f32(const float4 x, const float4 y, rae_f32x4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, y.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, y.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, y.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, y.w, acc, 0, 0, 0);
+    return acc;
+}
+__device__ __forceinline__ float4 load4_guard(const float* p, int k, int n, bool ok, bool vec) {
+    if (vec) return (ok && k < n) ? *reinterpret_cast<const float4*>(p + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v;
+    v.x = (ok && k < n) ? p[k] : 0.f;
+    v.y = (ok && k + 1 < n) ? p[k + 1] : 0.f;
+    v.z = (ok && k + 2 < n) ? p[k + 2] : 0.f;
+    v.w = (ok && k + 3 < n) ? p[k + 3] : 0.f;
+    return v;
+}
+
+__host__ __device__ inline int sp_cp_tasks(int l, int r) { return 2 * ((l + 15) / 16) * ((r + 15) / 16); }
+__host__ __device__ inline int sp_ctdw_tasks(int l, int m) { return ((l + 15) / 16) * ((m + 15) / 16); }
+
+// The two GEMMs: one 4-wave workgroup per 16 x 16 output tile; wave w takes the K chunks
+// c = w, w + 4, ... (16 deep each), four chunks' loads issued before their MFMAs, and the
+// four waves' accumulators are combined in LDS in wave order (deterministic).
+#define RAE_SPG_U 4
+__device__ __forceinline__ void sp_gemm_combine(rae_f32x4 acc, float* red, int lane, int w,
+                                                float out[4]) {
+    float4* r4 = reinterpret_cast<float4*>(red);
+    r4[w * 64 + lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (w == 0) {
+        float4 t = r4[lane];
+#pragma unroll
+        for (int ww = 1; ww < RAE_NWAVE; ++ww) {
+            const float4 u = r4[ww * 64 + lane];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        out[0] = t.x; out[1] = t.y; out[2] = t.z; out[3] = t.w;
+    }
+}
+
+// k_sp_cp: tile (example, i) of V1 or V2.  A = P (rows b, K = k), B = C^T (K = k, columns i):
+// both K-contiguous, one float4 per lane per 16-deep chunk.
+__device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
+    const int l = a.l, m = a.m, r = a.r;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nbt = (l + 15) / 16, nit = (r + 15) / 16;
+    const int which = task / (nbt * nit), t2 = task - which * nbt * nit;
+    const int bt = t2 / nit, it = t2 - bt * nit;
+    const int li = lane & 15, g = lane >> 4;
+    const int b = bt * 16 + li, i = it * 16 + li;
+    const bool bv = b < l, iv = i < r, vec = (m & 3) == 0;
+    const float* Pr = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec + a.lay.oP;
+    const float* Cr = (which ? a.C2 : a.C1) + (int64_t)(iv ? i : 0) * m;
+    rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nch = (m + 15) / 16;
+    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
+        float4 x[RAE_SPG_U], y[RAE_SPG_U];
+#pragma unroll
+        for (int u = 0; u < RAE_SPG_U; ++u) {
+            const int k = (c0 + u * RAE_NWAVE) * 16 + 4 * g;     // >= m past the last chunk
+            x[u] = load4_guard(Pr, k, m, bv, vec);
+            y[u] = load4_guard(Cr, k, m, iv, vec);
+        }
+#pragma unroll
+        for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+    }
+    float o[4];
+    sp_gemm_combine(acc, red, lane, w, o);
+    if (w != 0) return;
+    const int oV = which ? a.lay.oV2 : a.lay.oV1;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][i = li]
+        const int bo = bt * 16 + 4 * g + reg;
+        if (bo < l && iv) a.ex[(int64_t)(a.rank * l + bo) * a.lay.rec + oV + i] = o[reg];
+    }
+}
+
+// k_sp_ctdw: tile (example, k) of dP.  A = dw (rows b, K = i: one float4 per lane per chunk),
+// B = C (K = i rows, columns k: four strided scalars per lane); K runs over C1's then C2's i.
+__device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
+    const int l = a.l, m = a.m, r = a.r;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nkt = (m + 15) / 16;
+    const int bt = task / nkt, kt = task - bt * nkt;
+    const int li = lane & 15, g = lane >> 4;
+    const int b = bt * 16 + li, k = kt * 16 + li;
+    const bool bv = b < l, kv = k < m, vec = (r & 3) == 0;
+    const float* rec = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec;
+    const int kc = kv ? k : 0;
+    rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nci = (r + 15) / 16, nch = 2 * nci;
+    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
+        float4 x[RAE_SPG_U], y[RAE_SPG_U];
+#pragma unroll
+        for (int u = 0; u < RAE_SPG_U; ++u) {
+            const int c = c0 + u * RAE_NWAVE;
+            const bool cv = c < nch;
+            const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
+            const float* Dw = rec + (which ? a.lay.odw2 : a.lay.odw1);
+            const float* Cm = which ? a.C2 : a.C1;
+            x[u] = load4_guard(Dw, i, r, bv && cv, vec);
+            y[u].x = (cv && kv && i < r) ? Cm[(int64_t)i * m + kc] : 0.f;
+            y[u].y = (cv && kv && i + 1 < r) ? Cm[(int64_t)(i + 1) * m + kc] : 0.f;
+            y[u].z = (cv && kv && i + 2 < r) ? Cm[(int64_t)(i + 2) * m + kc] : 0.f;
+            y[u].w = (cv && kv && i + 3 < r) ? Cm[(int64_t)(i + 3) * m + kc] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+    }
+    float o[4];
+    sp_gemm_combine(acc, red, lane, w, o);
+    if (w != 0) return;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][k = li]
+        const int bo = bt * 16 + 4 * g + reg;
+        if (bo < l && kv) a.dPs[(int64_t)bo * m + k] = o[reg];
+    }
+}
+
+template <bool V4>
+__device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
+    const DynDims Dm(a);
+    const int m = Dm.m, r = Dm.r, s = Dm.s, NR = 1 + 2 * s, NJ = 2 + 2 * s;
+    ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
+    const int bg = a.rank * a.l + bl;
+    const int64_t ex = g * (int64_t)a.L + bg;
+    const int64_t col = a.neg_mode ? ex : (int64_t)bg;
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    RAE_STAMP(a, 0);
+    load_ids(a, Dm, ex, col, S);
+    const float H = rec[a.lay.oloss];
+    __syncthreads();
+    RAE_STAMP(a, 1);
+    if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
+    gather_rows_dma<V4>(a, Dm, S, NR, 1);
+    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
+        S.swC1[i] = rec[a.lay.oV1 + i];
+        S.swC2[i] = rec[a.lay.oV2 + i];
+    }
+    __syncthreads();                                      // the A-row DMA has landed
+    RAE_STAMP(a, 2);
+    sp_dots<V4>(Dm, S);
+    __syncthreads();
+    RAE_STAMP(a, 3);
+    sp_coefficients(a, Dm, S, H);
+    __syncthreads();
+    RAE_STAMP(a, 4);
+    sp_weighted_rows<V4>(Dm, S);
+    __syncthreads();
+    RAE_STAMP(a, 5);
+    const float dl = S.scoef[0], dr = S.scoef[1];
+    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
+        rec[a.lay.odw1 + i] = S.sdw1[i];
+        rec[a.lay.odw2 + i] = S.sdw2[i];
+        rec[a.lay.oG1 + i] = dl * S.swC1[i] + dr * S.swC2[i];   // A[e1]: left and right
+    }
+    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
+        const float* c = S.scoef + 3 * j;
+        const float cj = j == 0 ? 1.f : (j == 1 ? 0.f : (j < 2 + s ? c[0] : c[1]));
+        rec[a.lay.ocoef + 2 * j] = cj;
+        rec[a.lay.ocoef + 2 * j + 1] = c[2];
+    }
+    if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
+    RAE_STAMP(a, 6);
+    RAE_STAMP(a, 7);
+}
+
+// k_sp_fin: dS_k = P_k((dP_k - sum P dP) + ce (z_k - sum P z)), as softmax_backward
+__device__ void sp_split_fin(const StepArgs& a, int bl, float* red) {
+    const int m = a.m;
+    float* rec = a.ex + (int64_t)(a.rank * a.l + bl) * a.lay.rec;
+    const float* dP = a.dPs + (int64_t)bl * m;
+    const float ce = 2.f * a.alpha * a.invD;
+    float sd = 0.f, sz = 0.f;
+    for (int k = threadIdx.x; k < m; k += RAE_BT) {
+        const float p = rec[a.lay.oP + k];
+        sd += p * dP[k];
+        sz += p * rec[a.lay.odS + k];
+    }
+    sd = block_sum<RAE_BT>(sd, red);
+    sz = block_sum<RAE_BT>(sz, red + RAE_NWAVE);
+    for (int k = threadIdx.x; k < m; k += RAE_BT) {
+        const float p = rec[a.lay.oP + k];
+        rec[a.lay.odS + k] = p * ((dP[k] - sd) + ce * (rec[a.lay.odS + k] - sz));
+    }
+}
+
+}  // namespace rae

@@ -95,6 +95,7 @@ struct StepArgs {
     float* costs;
     float* gWs;          // dense W gradient scratch (reg_on only)
     float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
+    float* dPs;          // split SP forward (rae_sp_split.hpp): dP = dw1 C1 + dw2 C2 (l, m)
     float* mtV;          // bilinear: k_bil_mt partials over j-blocks (nblk, l, r4): M a2 / M y
     float* mtW;          //           ... over i-blocks: M^T a1 / M^T x
     int r4;              // align4(r): row stride of the partials

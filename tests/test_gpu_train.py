@@ -134,6 +134,34 @@ def test_synthetic_vs_oracle(built_lib, cuda_dev, shape):
     _assert_params_close(_params(ind), tr.params, "synthetic")
 
 
+@pytest.mark.parametrize("shape", [
+    dict(N=400, d=300, m=8, r=16, s=4, l=50, ntrue=4, force=True),
+    dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5, force=True),      # scalar path
+    dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10, force=True),
+    dict(N=200, d=3000, m=300, r=300, s=50, l=100, ntrue=10, epochs=1),  # C4 K/r/s: split by default
+], ids=["small", "odd", "c3shape", "c4shape"])
+def test_split_sp_forward_vs_oracle(built_lib, cuda_dev, shape, monkeypatch):
+    """The split SP forward (rae_sp_split.hpp: encoder, P.C^T GEMM, decoder, dw.C GEMM,
+    softmax backward as five kernels) against the float64 oracle, with the same tolerances as
+    the fused example kernel."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    if shape.get("force"):
+        monkeypatch.setenv("RAE_SPSPLIT", "1")
+    else:
+        monkeypatch.delenv("RAE_SPSPLIT", raising=False)
+    data, gold = synthetic_dataset(shape["N"], shape["d"], shape["ntrue"], seed=99)
+    m, r, s, l = shape["m"], shape["r"], shape["s"], shape["l"]
+    ep = shape.get("epochs", 2)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), ep, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "split", "sp", False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=2)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory("sp", data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "split")
+
+
 def test_bitwise_deterministic(built_lib, cuda_dev):
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer

@@ -99,6 +99,8 @@ def main():
     names = {"A-index": ["enumerate", "sort", "segment"], "W-index": ["enumerate", "sort", "segment"],
              "example": ["ids+C-cache", "encoder+gather", "C.P", "dots", "coef+dwC", "back+softmax",
                          "record"]}
+    if cfg["dec"] == "sp" and cfg["r"] * cfg["m"] > 32768:      # split forward: k_sp_dec's stamps
+        names["example"] = ["ids", "A-DMA+V", "dots", "coef", "weighted-rows", "record", "-"]
     spans = []
     for kind, sl in kinds.items():
         if sl.stop <= sl.start:
