@@ -493,37 +493,34 @@ __device__ __forceinline__ void sp_weighted_rows(const D& Dm, ExampleSmem& S) {
 }
 
 // dot products of the example's A rows with wC1 / wC2 (S.srows, S.swC1, S.swC2 -> S.sdots):
-// row rho on wave rho % NW; lanes over vector columns
+// one thread per dot, the whole row from LDS (wC broadcast), no cross-lane reductions --
+// one wave_sum per row serialised ~13 reductions per wave at C4 (4 us for 101 rows)
 template <bool V4, class D>
 __device__ __forceinline__ void sp_dots(const D& Dm, ExampleSmem& S) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
     const int r = Dm.r, s = Dm.s, NR = 1 + 2 * s, r4 = align4(r);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    {
-        const int rv = r / VW, r4v = r4 / VW;
-        const VT* Rv = reinterpret_cast<const VT*>(S.srows);
-        const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
-        const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
-        for (int rho = w; rho < NR; rho += RAE_FNW) {
-            const VT* wv = rho > s ? W2 : W1;      // rows 1..s: neg1, s+1..2s: neg2
-            float d1 = 0.f, d2 = 0.f;
-            for (int c = lane; c < rv; c += RAE_WAVE) {
-                const VT x = Rv[rho * r4v + c];
-                d1 += vdot(x, wv[c]);
-                if (rho == 0) d2 += vdot(x, W2[c]);
-            }
-            d1 = wave_sum(d1);
-            if (rho == 0) d2 = wave_sum(d2);
-            if (lane == 0) {
-                if (rho == 0) {
-                    S.sdots[0] = d1;     // left  = <wC1, A[e1]>
-                    S.sdots[1] = d2;     // right = <wC2, A[e1]>
-                } else {
-                    S.sdots[rho + 1] = d1;   // record j = rho + 1
-                }
-            }
+    const int rv = r / VW, r4v = r4 / VW;
+    const VT* Rv = reinterpret_cast<const VT*>(S.srows);
+    const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
+    const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
+    for (int t = threadIdx.x; t <= NR; t += RAE_FBT) {
+        // t = 0: <wC1, A[e1]> (left); t = NR: <wC2, A[e1]> (right); else row t with wC1
+        // (rows 1..s: neg1) or wC2 (rows s+1..2s: neg2)
+        const int rho = t == NR ? 0 : t;
+        const VT* wv = (t == NR || rho > s) ? W2 : W1;
+        const VT* x = Rv + rho * r4v;
+        float d0 = 0.f, d1 = 0.f;
+        int c = 0;
+        for (; c + 2 <= rv; c += 2) {
+            d0 += vdot(x[c], wv[c]);
+            d1 += vdot(x[c + 1], wv[c + 1]);
         }
+        if (c < rv) d0 += vdot(x[c], wv[c]);
+        const float d = d0 + d1;
+        if (t == 0) S.sdots[0] = d;             // left  = <wC1, A[e1]>
+        else if (t == NR) S.sdots[1] = d;       // right = <wC2, A[e1]>
+        else S.sdots[t + 1] = d;                // record j = rho + 1
     }
 }
 
@@ -539,15 +536,20 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
         for (int t = lane; t < s; t += RAE_WAVE) {
             const float g1 = S.sdots[2 + t] + right + S.sAbv[2 + t];
             const float g2 = S.sdots[2 + s + t] + left + S.sAbv[2 + s + t];
-            const float dg1 = sigmoid(g1) * a.invD;
-            const float dg2 = sigmoid(g2) * a.invD;
+            // hardware transcendental forms (one exp per score; the fast path's): a single
+            // wave runs this block, so the libm sequences were its whole 1.7 us at C4
+            float sg1, sp1, sg2, sp2;
+            sigmoid_softplus(g1, sg1, sp1);
+            sigmoid_softplus(g2, sg2, sp2);
+            const float dg1 = sg1 * a.invD;
+            const float dg2 = sg2 * a.invD;
             float* c1 = S.scoef + 3 * (2 + t);
             float* c2 = S.scoef + 3 * (2 + s + t);
             c1[0] = dg1; c1[1] = 0.f; c1[2] = dg1;
             c2[0] = 0.f; c2[1] = dg2; c2[2] = dg2;
             sdg1 += dg1;
             sdg2 += dg2;
-            sls += log_sigmoid(-g1) + log_sigmoid(-g2);
+            sls -= sp1 + sp2;                   // log sigmoid(-g) = -softplus(g)
         }
         sdg1 = wave_sum(sdg1);
         sdg2 = wave_sum(sdg2);
@@ -555,13 +557,16 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
         if (lane == 0) {
             const float one = left + right;
             const float u1 = one + S.sAbv[0], u2 = one + S.sAbv[1];
-            const float du1 = -sigmoid(-u1) * a.invD;
-            const float du2 = -sigmoid(-u2) * a.invD;
+            float su1, pu1, su2, pu2;               // sigmoid(-u), softplus(-u)
+            sigmoid_softplus(-u1, su1, pu1);
+            sigmoid_softplus(-u2, su2, pu2);
+            const float du1 = -su1 * a.invD;
+            const float du2 = -su2 * a.invD;
             const float dl = du1 + du2 + sdg2;     // d cost / d left
             const float dr = du1 + du2 + sdg1;     // d cost / d right
             S.scoef[0] = dl; S.scoef[1] = dr; S.scoef[2] = du1;
             S.scoef[3] = 0.f; S.scoef[4] = 0.f; S.scoef[5] = du2;
-            S.sred[32] = log_sigmoid(u1) + log_sigmoid(u2) + 2.f * H + sls;
+            S.sred[32] = -pu1 - pu2 + 2.f * H + sls;   // log sigmoid(u) = -softplus(-u)
         }
     }
 }
