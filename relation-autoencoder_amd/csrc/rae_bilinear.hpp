@@ -650,15 +650,18 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         for (int t = lane; t < s; t += RAE_WAVE) {
             const float g1 = S.dots[t] + sp2 + S.Abv[2 + t];
             const float g2 = S.dots[s + t] + sp1 + S.Abv[2 + s + t];
-            const float dg1 = sigmoid(g1) * a.invD;
-            const float dg2 = sigmoid(g2) * a.invD;
+            float sg1, spl1, sg2, spl2;           // hardware exp/log (rae_common.hpp)
+            sigmoid_softplus(g1, sg1, spl1);
+            sigmoid_softplus(g2, sg2, spl2);
+            const float dg1 = sg1 * a.invD;
+            const float dg2 = sg2 * a.invD;
             float* c1 = S.coef + 3 * (2 + t);
             float* c2 = S.coef + 3 * (2 + s + t);
             c1[0] = dg1; c1[1] = 0.f; c1[2] = dg1;
             c2[0] = 0.f; c2[1] = dg2; c2[2] = dg2;
             sdg1 += dg1;
             sdg2 += dg2;
-            sls += log_sigmoid(-g1) + log_sigmoid(-g2);
+            sls -= spl1 + spl2;                   // log sigmoid(-g) = -softplus(g)
         }
         sdg1 = wave_sum(sdg1);
         sdg2 = wave_sum(sdg2);
@@ -666,15 +669,18 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
         if (lane == 0) {
             const float one = S.dots[2 * s] + sp1 + sp2;
             const float u1 = one + S.Abv[0], u2 = one + S.Abv[1];
-            const float du1 = -sigmoid(-u1) * a.invD;
-            const float du2 = -sigmoid(-u2) * a.invD;
+            float su1, pu1, su2, pu2;             // sigmoid(-u), softplus(-u)
+            sigmoid_softplus(-u1, su1, pu1);
+            sigmoid_softplus(-u2, su2, pu2);
+            const float du1 = -su1 * a.invD;
+            const float du2 = -su2 * a.invD;
             const float dOne = du1 + du2;
             S.coef[0] = 0.f; S.coef[1] = 0.f; S.coef[2] = du1;
             S.coef[3] = 0.f; S.coef[4] = 0.f; S.coef[5] = du2;
             S.red[0] = dOne;
             S.red[1] = dOne + sdg2;      // c_a1: <wC1,a1> sits in one and every negTwo
             S.red[2] = dOne + sdg1;      // c_a2: <wC2,a2> sits in one and every negOne
-            S.red[32] = log_sigmoid(u1) + log_sigmoid(u2) + 2.f * H + sls;
+            S.red[32] = -pu1 - pu2 + 2.f * H + sls;   // log sigmoid(u) = -softplus(-u)
         }
     }
     __syncthreads();

@@ -132,16 +132,6 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // Stable forms of Theano's rewritten log(sigmoid(x)) -> -softplus(-x) and sigmoid.
-__device__ __forceinline__ float softplus(float x) {
-    return x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
-}
-__device__ __forceinline__ float log_sigmoid(float x) { return -softplus(-x); }
-__device__ __forceinline__ float sigmoid(float x) {
-    if (x >= 0.f) { const float z = expf(-x); return 1.f / (1.f + z); }
-    const float z = expf(x);
-    return z / (1.f + z);
-}
-
 // One exp shared by sigmoid(x) and softplus(x) = log(1 + e^x), hardware transcendental
 // forms (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): e = exp(-|x|),
 //   sigmoid(x)  = x >= 0 ? 1/(1+e) : e/(1+e)

@@ -345,15 +345,15 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
             for (int k = lane; k < m; k += RAE_WAVE) mx = fmaxf(mx, sS[k]);
             mx = wave_max(mx);
             float se = 0.f;
-            for (int k = lane; k < m; k += RAE_WAVE) se += expf(sS[k] - mx);
+            for (int k = lane; k < m; k += RAE_WAVE) se += __expf(sS[k] - mx);
             se = wave_sum(se);
-            const float lse = logf(se);
+            const float lse = __logf(se);
             float hp = 0.f;
             for (int k = lane; k < mp; k += RAE_WAVE) {
                 float z = 0.f, p = 0.f;
                 if (k < m) {
                     z = sS[k] - mx;
-                    p = expf(z) / se;
+                    p = __expf(z) / se;
                 }
                 S.sZ[k] = z;
                 S.sP[k] = p;
@@ -367,15 +367,15 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         for (int k = threadIdx.x; k < m; k += RAE_FBT) mx = fmaxf(mx, sS[k]);
         mx = block_max<RAE_FBT>(mx, S.sred);
         float se = 0.f;
-        for (int k = threadIdx.x; k < m; k += RAE_FBT) se += expf(sS[k] - mx);
+        for (int k = threadIdx.x; k < m; k += RAE_FBT) se += __expf(sS[k] - mx);
         se = block_sum<RAE_FBT>(se, S.sred + 8);
-        const float lse = logf(se);
+        const float lse = __logf(se);
         float hp = 0.f;
         for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
             float z = 0.f, p = 0.f;
             if (k < m) {
                 z = sS[k] - mx;
-                p = expf(z) / se;
+                p = __expf(z) / se;
             }
             S.sZ[k] = z;
             S.sP[k] = p;
