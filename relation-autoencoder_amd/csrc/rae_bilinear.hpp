@@ -374,7 +374,9 @@ __device__ void bil_gemm_dp_bf16(const StepArgs& a, int t, int lane) {
 // per (i, 32-wide j step) and reused MT times.  Partial sums per i-block -> dPpart, summed
 // in block order by bil_finish (deterministic).  Shapes: r <= 32 NJS, m <= 16 MT,
 // r % 4 == m % 4 == 0.
+#ifndef RAE_IB2
 #define RAE_IB2 2    // i rows per k_bil_dp2 workgroup (the q-loop selects x/a1 for q < 2)
+#endif
 // threads per k_bil_dp2 workgroup: 512 for C5's <7, 7> (its 7 example tiles in one round);
 // <8, 8> needs more than the 256 VGPRs an 8-wave workgroup allows, so it keeps 4 waves
 template <int NJS, int MT>
