@@ -639,6 +639,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const int64_t nbi_mt = (c.embed + RAE_MTI - 1) / RAE_MTI, nbj_mt = (c.embed + RAE_MTJ - 1) / RAE_MTJ;
     const size_t o_mtv = bil ? take(4ull * nbj_mt * c.batch_size * a.r4) : 0;
     const size_t o_mtw = bil ? take(4ull * nbi_mt * c.batch_size * a.r4) : 0;
+    // dP inside the second k_bil_mt pass (bf16 blocks; RAE_MTDP=0 keeps k_bil_dp2 / k_bil_dp)
+    const char* mtdpenv = getenv("RAE_MTDP");
+    const bool mtdp = bil && c.mfma_bf16 && c.relations <= 128 && !(mtdpenv && mtdpenv[0] == '0');
+    a.nmtp = (int)(nbi_mt * nbj_mt);
+    const size_t o_mtp = mtdp ? take(4ull * a.nmtp * c.batch_size * c.relations) : 0;
     // split SP forward (rae_sp_split.hpp) for runtime shapes whose decoder matrices stream
     // through every example's workgroup (r*m > RAE_SPLIT_RM; C4: 90 k); RAE_SPSPLIT=0/1 forces
     const char* splitenv = getenv("RAE_SPSPLIT");
@@ -675,6 +680,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.dPs = p->sp_split ? reinterpret_cast<float*>(p->ws + o_dps) : nullptr;
     a.mtV = bil ? reinterpret_cast<float*>(p->ws + o_mtv) : nullptr;
     a.mtW = bil ? reinterpret_cast<float*>(p->ws + o_mtw) : nullptr;
+    a.mtP = mtdp ? reinterpret_cast<float*>(p->ws + o_mtp) : nullptr;
     a.facT = a.bf16 ? reinterpret_cast<float*>(p->ws + o_fac) : nullptr;
     a.pfrag = a.bf16 ? reinterpret_cast<uint4*>(p->ws + o_pfr) : nullptr;
     a.err = p->d_err;
@@ -797,6 +803,7 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         RAE_LAUNCH(p, (k_forward<false, DynDims>), gr, bt, p->smem_fwd, st, a);
 }
 
+static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st);
 template <bool V4>
 static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
@@ -807,6 +814,11 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
     if (p->mt_bf16) RAE_LAUNCH(p, k_bil_mt<true>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
     else RAE_LAUNCH(p, k_bil_mt<false>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
+    if (!a.mtP) launch_fwd_dp(p, a, st);              // else dP came with the second pass
+    RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_FINT), 0, st, a);
+}
+
+static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const int gd = ceil_div(bil_dp_tasks(a.l, a.m, a.nib), RAE_NWAVE);
     const size_t lds77 = dp2_lds_bytes<7, 7>(), lds88 = dp2_lds_bytes<8, 8>();
     if (p->dp2 == 1)
@@ -817,7 +829,6 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
         RAE_LAUNCH(p, k_bil_dp<true>, dim3(gd), dim3(RAE_BT), 0, st, a);
     else
         RAE_LAUNCH(p, k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
-    RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_FINT), 0, st, a);
 }
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {

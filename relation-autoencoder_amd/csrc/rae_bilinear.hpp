@@ -194,8 +194,11 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
         const float* erb = a.ex + (int64_t)(a.rank * l + (bv ? bb : 0)) * a.lay.rec;
         const float* Pa = erb + a.lay.oP;
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        // masked by a multiply, not a select: the compiler turns "load, then zero" into a load
+        // through a zeroed scratch slot when registers are tight (the address is always valid)
+        const float okv = (bv && j0 + 4 * g < r) ? 1.f : 0.f;
         float4 cv = *reinterpret_cast<const float4*>(erb + ov + (j0 + 4 * g < r ? j0 + 4 * g : 0));
-        if (!bv || j0 + 4 * g >= r) cv = z4;
+        cv.x *= okv; cv.y *= okv; cv.z *= okv; cv.w *= okv;
         float cw[RAE_MTI];
 #pragma unroll
         for (int q = 0; q < RAE_MTI / 4; ++q) {
@@ -272,6 +275,76 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                 *reinterpret_cast<float4*>(a.mtW + ((int64_t)it * l + bb) * a.r4 + j0 + 4 * g) = wacc;
         }
         RAE_MT_STAMP(5);
+        if constexpr (BF16) {
+            if (pass == 1 && a.mtP) {
+                // the block's share of dP_b[k] = sum_ij U_b[i][j] R[i][j][k], U = x a2^T + a1 y^T,
+                // from the same staged block (k_bil_dp2's contraction without another read of
+                // R): D[b][k] over K = the block's 128 (i, j) pairs = its LDS rows; A = U (lane
+                // (li, g): example bb, pairs 32 ks + 8g .. +7 = row i0 + 2 ks + g/2, columns
+                // j0 + 8 (g&1) .. +7), B = 8 rows of the LDS image at column k
+                const int jh = j0 + 8 * (g & 1);
+                float a2v[8], yv[8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int j = jh + 4 * h;                // r4 padding of the record is zero
+                    const bool ok = bv && j < r;
+                    const int jc = j < r ? j : 0;
+                    const float4 va = *reinterpret_cast<const float4*>(erb + a.lay.oA2 + jc);
+                    const float4 vy = *reinterpret_cast<const float4*>(erb + a.lay.oY + jc);
+                    a2v[4 * h + 0] = ok ? va.x : 0.f; a2v[4 * h + 1] = ok ? va.y : 0.f;
+                    a2v[4 * h + 2] = ok ? va.z : 0.f; a2v[4 * h + 3] = ok ? va.w : 0.f;
+                    yv[4 * h + 0] = ok ? vy.x : 0.f; yv[4 * h + 1] = ok ? vy.y : 0.f;
+                    yv[4 * h + 2] = ok ? vy.z : 0.f; yv[4 * h + 3] = ok ? vy.w : 0.f;
+                }
+                // x / a1 at rows i0 + 2 ks + g/2, ks = 0..3 (named: the K-step loop is rolled)
+                // (unconditional loads of clamped addresses, then selects: a conditional load
+                // becomes a flat load through a zeroed scratch slot)
+                const int ib = i0 + (g >> 1);
+                const float* px = erb + a.lay.oX;
+                const float* pc = erb + a.lay.oA1;
+                const int q0 = min(ib, r - 1), q1 = min(ib + 2, r - 1), q2 = min(ib + 4, r - 1),
+                          q3 = min(ib + 6, r - 1);
+                const float lx0 = px[q0], lx1 = px[q1], lx2 = px[q2], lx3 = px[q3];
+                const float lc0 = pc[q0], lc1 = pc[q1], lc2 = pc[q2], lc3 = pc[q3];
+                const float x0 = (bv && ib < r) ? lx0 : 0.f, c0 = (bv && ib < r) ? lc0 : 0.f;
+                const float x1 = (bv && ib + 2 < r) ? lx1 : 0.f, c1 = (bv && ib + 2 < r) ? lc1 : 0.f;
+                const float x2 = (bv && ib + 4 < r) ? lx2 : 0.f, c2 = (bv && ib + 4 < r) ? lc2 : 0.f;
+                const float x3 = (bv && ib + 6 < r) ? lx3 : 0.f, c3 = (bv && ib + 6 < r) ? lc3 : 0.f;
+                const int nkt = (m + 15) / 16;               // <= 8 (m <= 128)
+                const __bf16* lb = reinterpret_cast<const __bf16*>(smem);
+                rae_bf4 dacc[8];
+#pragma unroll
+                for (int kt = 0; kt < 8; ++kt) dacc[kt] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+                for (int ks = 0; ks < 4; ++ks) {             // rolled: one K step's fragments live
+                    const float xk = (ks & 2) ? ((ks & 1) ? x3 : x2) : ((ks & 1) ? x1 : x0);
+                    const float ak = (ks & 2) ? ((ks & 1) ? c3 : c2) : ((ks & 1) ? c1 : c0);
+                    rae_bf16x8 ua;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) ua[e] = (__bf16)(xk * a2v[e] + ak * yv[e]);
+                    const __bf16* lr = lb + (ks * 32 + 8 * g) * ST + li;
+#pragma unroll
+                    for (int kt = 0; kt < 8; ++kt) {
+                        if (kt >= nkt) break;
+                        rae_bf16x8 rb;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) rb[e] = lr[e * ST + kt * 16];
+                        dacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, rb, dacc[kt], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int kt = 0; kt < 8; ++kt) {
+                    if (kt >= nkt) break;
+                    const int k = kt * 16 + li;
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) {     // D[b = 4g + reg][k = li]
+                        const int bo = bt * 16 + 4 * g + reg;
+                        if (bo < l && k < m)
+                            a.mtP[((int64_t)blockIdx.x * l + bo) * m + k] = dacc[kt][reg];
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -779,17 +852,21 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, fl
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     const float ce = 2.f * a.alpha * a.invD;      // entropy term, centred form (softmax_backward)
     const int NS = max(1, RAE_FINT / m);
+    // dP partials: per M-tile block of the second k_bil_mt pass (mtP), or per row block of
+    // k_bil_dp / k_bil_dp2 (dPpart)
+    const float* pbase = a.mtP ? a.mtP : a.dPpart;
+    const int npart = a.mtP ? a.nmtp : a.nib;
     for (int e = threadIdx.x; e < NS * m; e += RAE_FINT) {
         const int sp = e / m, k = e - sp * m;
-        const float* pp = a.dPpart + (int64_t)bl * m + k;
+        const float* pp = pbase + (int64_t)bl * m + k;
         const int64_t st = (int64_t)l * m;
         float t0 = 0.f, t1 = 0.f;
         int ib = sp;
-        for (; ib + NS < a.nib; ib += 2 * NS) {
+        for (; ib + NS < npart; ib += 2 * NS) {
             t0 += pp[ib * st];
             t1 += pp[(ib + NS) * st];
         }
-        if (ib < a.nib) t0 += pp[ib * st];
+        if (ib < npart) t0 += pp[ib * st];
         sdp[e] = t0 + t1;
     }
     mt_sums_split<RAE_FINT>(a, bl, smt, smt + 1024, smt + 2048, smt + 3072);

@@ -98,6 +98,8 @@ struct StepArgs {
     float* dPs;          // split SP forward (rae_sp_split.hpp): dP = dw1 C1 + dw2 C2 (l, m)
     float* mtV;          // bilinear: k_bil_mt partials over j-blocks (nblk, l, r4): M a2 / M y
     float* mtW;          //           ... over i-blocks: M^T a1 / M^T x
+    float* mtP;          //           dP partials of the second pass, per block (nmtp, l, m)
+    int nmtp;            //           blocks of a k_bil_mt pass
     int r4;              // align4(r): row stride of the partials
     int nib;             // bilinear: number of i-blocks of the dP contraction
     int bf16;            // bilinear: bf16 MFMA operands (fp32 accumulation) for the R GEMMs

@@ -342,6 +342,7 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
     from rae.inducer import ReconstructInducer
     m, r, s, l = shape
     out = []
+    monkeypatch.setenv("RAE_MTDP", "0")       # dP from k_bil_dp2 / k_bil_dp, not k_bil_mt
     for flag in ("1", "0"):
         monkeypatch.setenv("RAE_DP2", flag)
         # two batches: longer runs amplify the summation-order difference chaotically
@@ -352,6 +353,32 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
         ind.learn(verbose=False)
         out.append((_params(ind), np.array(ind.epoch_costs)))
     # the per-batch costs drift with the parameters (up to 2.6e-5 relative seen)
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-4, atol=2e-6)
+    for k in out[0][0]:
+        a, b = out[0][0][k], out[1][0][k]
+        rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
+        assert rel < 5e-4, f"{k}: relative distance {rel:.3e}"
+
+
+@pytest.mark.parametrize("shape", [(100, 200, 20, 100), (60, 96, 5, 40), (20, 50, 3, 30)],
+                         ids=["c5", "padded", "ragged"])
+@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
+def test_bf16_dp_in_mtile_pass_agrees(built_lib, cuda_dev, dec, shape, monkeypatch):
+    """dP computed inside the second k_bil_mt pass (per 8x16 block of R, partials summed by
+    k_bil_fin) against k_bil_dp2 / k_bil_dp (RAE_MTDP=0): the same bf16 operands, another fp32
+    summation order -> two batches agree to 5e-4 relative (as test_bf16_dp_kernels_agree)."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = shape
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RAE_MTDP", flag)
+        data, gold = synthetic_dataset(2 * l, 2000, 10, seed=99)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0,
+                                 0.0, "adagrad", "mtdp", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True)
+        ind.learn(verbose=False)
+        out.append((_params(ind), np.array(ind.epoch_costs)))
     np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-4, atol=2e-6)
     for k in out[0][0]:
         a, b = out[0][0][k], out[1][0][k]
