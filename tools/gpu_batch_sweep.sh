@@ -10,7 +10,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 for b in $SIZES; do
-  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-label-pass --batch-size $b \
+  EXTRA=""; [ $b -ge 4096 ] && EXTRA="--steps 64 --warmup 16"     # an epoch has N/b batches
+  timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-label-pass --batch-size $b $EXTRA \
       > $O/bench_l$b.json 2> $O/bench_l$b.err || { echo bench l=$b failed; tail -20 $O/bench_l$b.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$O/bench_l$b.json'))

@@ -21,4 +21,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/c5mfma/stats -o 
 cd $R
 python3 tools/pmc_mfma.py $O/c5mfma/pmc --stats $(find $O/c5mfma/stats -name "*kernel_stats.csv" | head -1) --out $O/c5mfma/pmc_mfma.json | grep -B1 -A7 "k_bil_mt\|k_bil_dp2\|k_bil_rows" | head -60
 # batch sweep (global batch on one GPU: the replicated update's cost at G ranks), 8192 last
-bash tools/gpu_batch_sweep.sh $TAG/sweep 200 400 800 1024 1600 8192 || exit 1
+bash tools/gpu_batch_sweep.sh $TAG/sweep 100 400 800 1024 1600 8192 || exit 1
