@@ -860,14 +860,15 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, fl
         const int sp = e / m, k = e - sp * m;
         const float* pp = pbase + (int64_t)bl * m + k;
         const int64_t st = (int64_t)l * m;
-        float t0 = 0.f, t1 = 0.f;
+        // eight independent chains (fixed order): the loads of eight partials issue together
+        float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         int ib = sp;
-        for (; ib + NS < npart; ib += 2 * NS) {
-            t0 += pp[ib * st];
-            t1 += pp[(ib + NS) * st];
+        for (; ib + 7 * NS < npart; ib += 8 * NS) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] += pp[(ib + u * NS) * st];
         }
-        if (ib < npart) t0 += pp[ib * st];
-        sdp[e] = t0 + t1;
+        for (int u = 0; ib < npart; ib += NS, ++u) t[u] += pp[ib * st];
+        sdp[e] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
     mt_sums_split<RAE_FINT>(a, bl, smt, smt + 1024, smt + 2048, smt + 3072);
     __syncthreads();
