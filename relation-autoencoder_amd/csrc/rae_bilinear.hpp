@@ -112,10 +112,13 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
     const int KP = (m + 31) / 32 * 32;
     return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 : (size_t)RAE_MTI * RAE_MTJ * m * 4;
 }
-#ifdef RAE_STAMPS      // pass 0 only, past the per-example stamp region (l <= 1024)
+#ifndef RAE_MT_STAMP_PASS
+#define RAE_MT_STAMP_PASS 0
+#endif
+#ifdef RAE_STAMPS      // one pass only, past the per-example stamp region (l <= 1024)
 #define RAE_MT_STAMP(slot)                                                                      \
     do {                                                                                        \
-        if (a.stamps && pass == 0 && threadIdx.x == 0)                                          \
+        if (a.stamps && pass == RAE_MT_STAMP_PASS && threadIdx.x == 0)                          \
             a.stamps[16384 + (size_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
@@ -333,12 +336,16 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                     }
                 }
 #pragma unroll
+                RAE_MT_STAMP(6);
                 for (int kt = 0; kt < 8; ++kt) {
                     if (kt >= nkt) break;
                     const int k = kt * 16 + li;
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg) {     // D[b = 4g + reg][k = li]
                         const int bo = bt * 16 + 4 * g + reg;
+#ifdef RAE_MT_NODPST      // diagnostic: dP computed, not stored
+                        if (a.lr == -12345.f)
+#endif
                         if (bo < l && k < m)
                             a.mtP[((int64_t)blockIdx.x * l + bo) * m + k] = dacc[kt][reg];
                     }

@@ -50,6 +50,7 @@ def main():
     per = []
     vw = []
     nvw = ((cfg["r"] + 7) // 8) * ((cfg["r"] + 15) // 16)
+    NSLOT = 7 if "RAE_MT_STAMP_PASS=1" in os.environ.get("RAE_VARIANT", "") else 6
     for it in range(args.iters):
         bf = torch.zeros(16384 + nvw * 8, dtype=torch.int64, device=dev)
         lib.rae_debug_stamps(eng.plan, C.c_void_p(bf.data_ptr()), 1)
@@ -58,7 +59,7 @@ def main():
         lib.rae_step_update_at(eng.plan, 20 + it, st)
         torch.cuda.synchronize()
         allb = bf.cpu().numpy()
-        v = allb[16384:16384 + nvw * 8].reshape(nvw, 8).astype(np.float64)[:, :6] / 100.0
+        v = allb[16384:16384 + nvw * 8].reshape(nvw, 8).astype(np.float64)[:, :NSLOT] / 100.0
         vw.append(np.concatenate([v[:, :1] - v[:, 0].min(), np.diff(v, axis=1)], axis=1))
         f = allb[:gf * 16].reshape(gf, 16).astype(np.float64)[:, :7] / 100.0   # -> us
         t0 = f[:, 0].min()
@@ -69,8 +70,8 @@ def main():
     print("  " + "  ".join(f"{c} {np.median(per[:, i]):.2f}/{per[:, i].max():.2f}"
                            for i, c in enumerate(cols)))
     vw = np.concatenate(vw)
-    vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write"]
-    print(f"k_bil_mt pass 0 ({nvw} workgroups, wave 0 of each), median/max us per phase:")
+    vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write", "dP"][:NSLOT]
+    print(f"k_bil_mt pass {1 if NSLOT == 7 else 0} ({nvw} workgroups, wave 0 of each), median/max us per phase:")
     print("  " + "  ".join(f"{c} {np.median(vw[:, i]):.2f}/{vw[:, i].max():.2f}"
                            for i, c in enumerate(vcols)))
 
