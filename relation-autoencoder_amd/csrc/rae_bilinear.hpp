@@ -335,8 +335,8 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                         dacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, rb, dacc[kt], 0, 0, 0);
                     }
                 }
-#pragma unroll
                 RAE_MT_STAMP(6);
+#pragma unroll
                 for (int kt = 0; kt < 8; ++kt) {
                     if (kt >= nkt) break;
                     const int k = kt * 16 + li;

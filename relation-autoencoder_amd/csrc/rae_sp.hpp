@@ -493,8 +493,9 @@ __device__ __forceinline__ void sp_weighted_rows(const D& Dm, ExampleSmem& S) {
 }
 
 // dot products of the example's A rows with wC1 / wC2 (S.srows, S.swC1, S.swC2 -> S.sdots):
-// one thread per dot, the whole row from LDS (wC broadcast), no cross-lane reductions --
-// one wave_sum per row serialised ~13 reductions per wave at C4 (4 us for 101 rows)
+// 16 lanes per dot (strided columns, then one 16-lane DPP sum), every dot at once -- one
+// wave_sum per row serialised ~13 reductions per wave at C4, one thread per dot serialised
+// r LDS reads per thread at C2 (fp32 rows)
 template <bool V4, class D>
 __device__ __forceinline__ void sp_dots(const D& Dm, ExampleSmem& S) {
     typedef typename VecT<V4>::T VT;
@@ -504,23 +505,24 @@ __device__ __forceinline__ void sp_dots(const D& Dm, ExampleSmem& S) {
     const VT* Rv = reinterpret_cast<const VT*>(S.srows);
     const VT* W1 = reinterpret_cast<const VT*>(S.swC1);
     const VT* W2 = reinterpret_cast<const VT*>(S.swC2);
-    for (int t = threadIdx.x; t <= NR; t += RAE_FBT) {
-        // t = 0: <wC1, A[e1]> (left); t = NR: <wC2, A[e1]> (right); else row t with wC1
-        // (rows 1..s: neg1) or wC2 (rows s+1..2s: neg2)
-        const int rho = t == NR ? 0 : t;
-        const VT* wv = (t == NR || rho > s) ? W2 : W1;
-        const VT* x = Rv + rho * r4v;
-        float d0 = 0.f, d1 = 0.f;
-        int c = 0;
-        for (; c + 2 <= rv; c += 2) {
-            d0 += vdot(x[c], wv[c]);
-            d1 += vdot(x[c + 1], wv[c + 1]);
+    const int ndot = NR + 1;
+    for (int base = 0; base < ndot * 16; base += RAE_FBT) {     // uniform trip count
+        const int idx = base + threadIdx.x, t = idx >> 4, q = idx & 15;
+        float d = 0.f;
+        if (t < ndot) {
+            // t = 0: <wC1, A[e1]> (left); t = NR: <wC2, A[e1]> (right); else row t with wC1
+            // (rows 1..s: neg1) or wC2 (rows s+1..2s: neg2)
+            const int rho = t == NR ? 0 : t;
+            const VT* wv = (t == NR || rho > s) ? W2 : W1;
+            const VT* x = Rv + rho * r4v;
+            for (int c = q; c < rv; c += 16) d += vdot(x[c], wv[c]);
         }
-        if (c < rv) d0 += vdot(x[c], wv[c]);
-        const float d = d0 + d1;
-        if (t == 0) S.sdots[0] = d;             // left  = <wC1, A[e1]>
-        else if (t == NR) S.sdots[1] = d;       // right = <wC2, A[e1]>
-        else S.sdots[t + 1] = d;                // record j = rho + 1
+        d = group16_sum(d);
+        if (t < ndot && q == 0) {
+            if (t == 0) S.sdots[0] = d;             // left  = <wC1, A[e1]>
+            else if (t == NR) S.sdots[1] = d;       // right = <wC2, A[e1]>
+            else S.sdots[t + 1] = d;                // record j = rho + 1
+        }
     }
 }
 

@@ -290,6 +290,27 @@ def test_bf16_mfma_path_tracks_oracle(built_lib, cuda_dev, dec):
         assert rel < 2e-2, f"{k}: relative distance {rel:.3e}"
 
 
+@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
+def test_bf16_bilinear_bitwise_deterministic(built_lib, cuda_dev, dec):
+    """Two runs of the C5 path (bf16 MFMA, M-tile passes with dP, R-update kernel) give
+    bit-identical parameters and costs: every partial is combined in a fixed order.  (A
+    dynamically indexed MFMA accumulator once made the dP partials vary run to run.)"""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = 100, 200, 20, 100
+    out = []
+    for _ in range(2):
+        data, gold = synthetic_dataset(2 * l, 2000, 10, seed=99)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0,
+                                 0.0, "adagrad", "det", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True)
+        ind.learn(verbose=False)
+        out.append((_params(ind), list(ind.epoch_costs)))
+    assert out[0][1] == out[1][1]
+    for k in out[0][0]:
+        assert np.array_equal(out[0][0][k], out[1][0][k]), k
+
+
 def test_cursor_and_absolute_batch_launches_agree(built_lib, cuda_dev):
     # the two ways include/rae.h addresses a step's batch: a device cursor + offset
     # (rae_step_forward / rae_step_update) and the absolute index in the launch
