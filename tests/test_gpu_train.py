@@ -305,8 +305,8 @@ def test_bf16_bilinear_bitwise_deterministic(built_lib, cuda_dev, dec):
                                  0.0, "adagrad", "det", dec, False, True, False, 1.0,
                                  device=cuda_dev, graph_chunk=2, mfma_bf16=True)
         ind.learn(verbose=False)
-        out.append((_params(ind), list(ind.epoch_costs)))
-    assert out[0][1] == out[1][1]
+        out.append((_params(ind), np.array(ind.epoch_costs)))
+    assert np.array_equal(out[0][1], out[1][1])
     for k in out[0][0]:
         assert np.array_equal(out[0][0][k], out[1][0][k]), k
 
