@@ -108,9 +108,13 @@ __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
 #define RAE_MTT RAE_FBT   // threads per k_bil_mt workgroup (8 waves)
 #define RAE_MTW (RAE_MTT / RAE_WAVE)
 #define RAE_MT_SB 8       // float4 staging loads per thread in flight per round
+// bf16: the block image [(i,j)][KP + 8] and, for the dP contraction of the second pass, its
+// transpose [k][pairs + 8] (every B fragment one ds_read_b128)
+#define RAE_MT_TP (RAE_MTI * RAE_MTJ + 8)
 __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
     const int KP = (m + 31) / 32 * 32;
-    return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 : (size_t)RAE_MTI * RAE_MTJ * m * 4;
+    return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 + (size_t)KP * RAE_MT_TP * 2
+                : (size_t)RAE_MTI * RAE_MTJ * m * 4;
 }
 #ifndef RAE_MT_STAMP_PASS
 #define RAE_MT_STAMP_PASS 0
@@ -135,6 +139,8 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     const int it = blockIdx.x / nbj, jt = blockIdx.x - it * nbj;
     const int i0 = it * RAE_MTI, j0 = jt * RAE_MTJ;
     const int KP = (m + 31) / 32 * 32, ST = BF16 ? KP + 8 : m;   // row (i, j) stride in LDS
+    const bool tr = BF16 && pass == 1 && a.mtP != nullptr;        // stage the transpose too
+    __bf16* sT = reinterpret_cast<__bf16*>(smem) + RAE_MTI * RAE_MTJ * ST;
     RAE_MT_STAMP(0);
     // ---- stage: LDS row (ii, jj) = R[i0+ii][j0+jj][0..m); rows past r are zero
     if ((m & 3) == 0) {
@@ -162,6 +168,10 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                         q[0] = (__bf16)v[u].x; q[1] = (__bf16)v[u].y;
                         q[2] = (__bf16)v[u].z; q[3] = (__bf16)v[u].w;
                         *reinterpret_cast<bf4_t*>(reinterpret_cast<__bf16*>(smem) + row * ST + 4 * kq) = q;
+                        if (tr) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) sT[(4 * kq + c) * RAE_MT_TP + row] = q[c];
+                        }
                     } else {
                         *reinterpret_cast<float4*>(reinterpret_cast<float*>(smem) + row * ST + 4 * kq) = v[u];
                     }
@@ -173,14 +183,19 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
             const int row = e / m, k = e - row * m;
             const int i = i0 + row / RAE_MTJ, j = j0 + row % RAE_MTJ;
             const float x = (i < r && j < r) ? a.R3[((int64_t)i * r + j) * m + k] : 0.f;
-            if constexpr (BF16) reinterpret_cast<__bf16*>(smem)[row * ST + k] = (__bf16)x;
-            else reinterpret_cast<float*>(smem)[row * ST + k] = x;
+            if constexpr (BF16) {
+                reinterpret_cast<__bf16*>(smem)[row * ST + k] = (__bf16)x;
+                if (tr) sT[k * RAE_MT_TP + row] = (__bf16)x;
+            } else {
+                reinterpret_cast<float*>(smem)[row * ST + k] = x;
+            }
         }
     }
     if constexpr (BF16) {                      // zero K padding [m, KP)
         for (int e = tid; e < RAE_MTI * RAE_MTJ * (KP - m); e += RAE_MTT) {
             const int row = e / (KP - m), k = m + (e - row * (KP - m));
             reinterpret_cast<__bf16*>(smem)[row * ST + k] = (__bf16)0.f;
+            if (tr) sT[k * RAE_MT_TP + row] = (__bf16)0.f;
         }
     }
     RAE_MT_STAMP(1);
@@ -314,7 +329,6 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                 const float x2 = (bv && ib + 4 < r) ? lx2 : 0.f, c2 = (bv && ib + 4 < r) ? lc2 : 0.f;
                 const float x3 = (bv && ib + 6 < r) ? lx3 : 0.f, c3 = (bv && ib + 6 < r) ? lc3 : 0.f;
                 const int nkt = (m + 15) / 16;               // <= 8 (m <= 128)
-                const __bf16* lb = reinterpret_cast<const __bf16*>(smem);
                 rae_bf4 dacc[8];
 #pragma unroll
                 for (int kt = 0; kt < 8; ++kt) dacc[kt] = rae_bf4{0.f, 0.f, 0.f, 0.f};
@@ -325,13 +339,13 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                     rae_bf16x8 ua;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) ua[e] = (__bf16)(xk * a2v[e] + ak * yv[e]);
-                    const __bf16* lr = lb + (ks * 32 + 8 * g) * ST + li;
+                    // B[pair][k]: the transposed image, 8 consecutive pairs at column k
+                    const __bf16* lt = sT + li * RAE_MT_TP + ks * 32 + 8 * g;
 #pragma unroll
                     for (int kt = 0; kt < 8; ++kt) {
                         if (kt >= nkt) break;
-                        rae_bf16x8 rb;
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) rb[e] = lr[e * ST + kt * 16];
+                        const rae_bf16x8 rb =
+                            *reinterpret_cast<const rae_bf16x8*>(lt + kt * 16 * RAE_MT_TP);
                         dacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua, rb, dacc[kt], 0, 0, 0);
                     }
                 }

@@ -69,6 +69,14 @@ def main():
     print(f"k_bil_dec ({args.config}, {gf} workgroups), median/max us per phase:")
     print("  " + "  ".join(f"{c} {np.median(per[:, i]):.2f}/{per[:, i].max():.2f}"
                            for i, c in enumerate(cols)))
+    st = np.array([v[:, 0] for v in vw])          # per iteration: WG start offsets
+    print("k_bil_mt WG start offsets per iteration, p50/p90/p99/max us: " +
+          "  ".join(f"{np.percentile(x, 50):.2f}/{np.percentile(x, 90):.2f}/{np.percentile(x, 99):.2f}/{x.max():.2f}"
+                    for x in st))
+    late = np.concatenate([np.nonzero(x > 5.0)[0] for x in st])
+    if len(late):
+        print(f"  late WGs (> 5 us) by blockIdx: {sorted(set(late.tolist()))[:40]} ... (XCD = blockIdx % 8: "
+              f"{np.bincount(late % 8, minlength=8).tolist()})")
     vw = np.concatenate(vw)
     vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write", "dP"][:NSLOT]
     print(f"k_bil_mt pass {1 if NSLOT == 7 else 0} ({nvw} workgroups, wave 0 of each), median/max us per phase:")

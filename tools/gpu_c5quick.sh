@@ -2,7 +2,7 @@
 # C5: bilinear GPU tests, two bench lines, rocprof kernel stats.   usage: bash tools/gpu_c5quick.sh TAG
 set -o pipefail
 O=gpurun_out/${1:-c5q}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "rescal or hybrid or bil or bf16" > $O/gputests.log 2>&1 || { echo tests failed; tail -40 $O/gputests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "rescal or hybrid or bil or bf16 or bitwise" > $O/gputests.log 2>&1 || { echo tests failed; tail -40 $O/gputests.log; exit 1; }
 tail -1 $O/gputests.log
 for v in 1 2; do
   timeout -k 10 300 python3 -u bench.py --config c5 --no-cpu-baseline --no-label-pass --steps 256 --warmup 32 > $O/bench_$v.json 2> $O/bench_$v.err || { echo bench failed; tail -20 $O/bench_$v.err; exit 1; }
