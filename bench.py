@@ -480,7 +480,8 @@ def main():
                    "optimizer": "adagrad", "parallelism": f"dp{ws}",
                    "n_entities": data.get_arg_voc_size(),
                    "graph_chunk": args.graph_chunk if graphed else 1,
-                   "timed_graph_steps": timed_graphs},
+                   "timed_graph_steps": timed_graphs,
+                   "graph_batches": "absolute" if (graphed and eng.graph_absolute) else "cursor"},
         "roofline": roof,
         "kernels": kern,
         "kernel_us": {"forward": fwd_us, "update": upd_us,

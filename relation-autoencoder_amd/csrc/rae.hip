@@ -142,6 +142,10 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_index(StepArgs a, int64_t fir
     if (blockIdx.y == 2) build_batch_desc<RAE_FBT>(a, g, g % a.index_window);
     else build_batch_index<RAE_FBT>(a, g, g % a.index_window, blockIdx.y == 0, smem);
 }
+// the update's dispatch tables of the same batches (after k_build_index)
+__global__ __launch_bounds__(RAE_BT) void k_build_tasks(StepArgs a, int64_t first) {
+    build_batch_tasks<RAE_BT>(a, (first + blockIdx.x) % a.index_window);
+}
 
 __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
     return dec != RAE_DEC_RESCAL ? 2 * ((r + 15) / 16) * ((m + 15) / 16) : 0;
@@ -176,12 +180,12 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_UPD_WGCAP
 #define RAE_UPD_WGCAP 1536    // row-task workgroups: 6 per CU (24 waves) on 256 CUs
 #endif
-__host__ __device__ inline int64_t update_grid(int dec, int r, int m, int RA, int RW, int VCA, int VCW) {
+__host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
     const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
-    int64_t rows = ((int64_t)RA + RW + RAE_NWAVE - 1) / RAE_NWAVE;
+    int64_t rows = ((int64_t)TC + RAE_NWAVE - 1) / RAE_NWAVE;
     if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
-    return (int64_t)nT + nP + VCA + VCW + rows;
+    return (int64_t)nT + nP + NVC + rows;
 }
 
 template <int OPT, bool V4, int Q, bool BIL>
@@ -246,44 +250,44 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
 #endif
         return;
     }
-    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];   // records, rows, heavy, very heavy
-    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
-    const int HA = hA.z, HW = hW.z, LA = hA.y - hA.z, LW = hW.y - hW.z, VA = hA.w, VW = hW.w;
+    // row tasks from the slot's dispatch table (build_batch_tasks): the task entry and the
+    // table header are loaded together -- one round trip from wave start to the row's segment
     const int u = wg - nT - nP;
 #ifdef RAE_SKIP_ROWS
     return;                                                   // diagnostic: dense tasks alone
 #endif
-    if (u < VA + VW) {                                        // very heavy rows
-        RAE_FIRST(u < VA ? 8 : 9);
-        if (u < VA) wg_entity_row<OPT, V4, Q, BIL>(a, slot, u, w, lane, spart, sgb);
-        else wg_feature_row<OPT, V4, Q>(a, ex0, slot, u - VA, w, lane, spart);
+    const int4* thp = reinterpret_cast<const int4*>(a.thdr) + slot;
+    if (u < a.NVC) {                                          // very heavy rows
+        int4 seg = reinterpret_cast<const int4*>(a.vtask)[slot * a.NVC + u];
+        const int4 th = *thp;
+        if (u >= th.y) return;
+        const bool isA = seg.x >= 0;
+        RAE_FIRST(isA ? 8 : 9);
+        if (isA) {
+            wg_entity_row<OPT, V4, Q, BIL>(a, slot, seg, w, lane, spart, sgb);
+        } else {
+            seg.x = ~seg.x;
+            wg_feature_row<OPT, V4, Q>(a, ex0, slot, seg, w, lane, spart);
+        }
         RAE_WAVE_END();
         return;
     }
-    // row tasks: heavy A, heavy W, light A, light W; a wave with several tasks (large global
-    // batches: the grid's row part is capped near one resident wave per slot) loads its next
-    // task's segment while it works on the current one
-    const int nw = (gridDim.x - nT - nP - VA - VW) * RAE_NWAVE;
-    const int T = HA + HW + LA + LW;
-    auto seg_of = [&](int t, bool& isA) {
-        int x = t;
-        if (x < HA) { isA = true; }
-        else if ((x -= HA) < HW) { isA = false; }
-        else if ((x -= HW) < LA) { isA = true; x = a.RA - 1 - x; }
-        else { isA = false; x = a.RW - 1 - (x - LA); }
-        return row_segment(a, slot, isA, x);
-    };
-    int t = (u - VA - VW) * RAE_NWAVE + w;
-    bool isA = true, nA = true;
-    int4 seg = t < T ? seg_of(t, isA) : make_int4(0, 0, 0, 0);
+    // wave tasks: a wave with several (large global batches: the grid's row part is capped
+    // near one resident wave per slot) loads its next task's segment while it works on the
+    // current one
+    const int nw = (gridDim.x - nT - nP - a.NVC) * RAE_NWAVE;
+    const int4* tk = reinterpret_cast<const int4*>(a.task) + slot * a.TC;
+    int t = (u - a.NVC) * RAE_NWAVE + w;
+    int4 seg = tk[t < a.TC ? t : a.TC - 1];
+    const int T = thp->x;
     for (; t < T; t += nw) {
-        const int4 cur = seg;
-        const bool curA = isA;
-        if (t + nw < T) seg = seg_of(t + nw, nA);
-        RAE_FIRST(curA ? (t < HA ? 6 : 4) : (t < HA + HW ? 7 : 5));
+        int4 cur = seg;
+        if (t + nw < T) seg = tk[t + nw];
+        const bool curA = cur.x >= 0;
+        if (!curA) cur.x = ~cur.x;
+        RAE_FIRST((curA ? 4 : 5) + (cur.z - cur.y > RAE_HEAVY ? 2 : 0));
         if (curA) task_entity_row<OPT, V4, Q, BIL>(a, slot, cur, lane);
         else task_feature_row<OPT, V4, Q>(a, ex0, slot, cur, lane);
-        isA = nA;
         RAE_WAVE_END();
     }
 #undef RAE_FIRST
@@ -613,6 +617,15 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.VCA = a.RA / (RAE_VHEAVY + 1) + 1;       // very heavy rows per batch are fewer than this
     a.VCW = a.RW / (RAE_VHEAVY + 1) + 1;
     const size_t o_vrowA = take(16ull * W_ * a.VCA), o_vrowW = take(16ull * W_ * a.VCW);
+    // the update's dispatch table: every unique row is at most one task (TC = records), and
+    // NVC very heavy rows get a workgroup each (L/8 at least 32 -- the rest run as wave tasks)
+    a.TC = a.RA + a.RW;
+    {
+        const int nvc = L / 8 > 32 ? L / 8 : 32;
+        a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
+    }
+    const size_t o_thdr = take(16 * W_), o_task = take(16ull * W_ * a.TC);
+    const size_t o_vtask = take(16ull * W_ * a.NVC);
     {
         const int NJd = 2 + 2 * c.neg_samples;
         int cap = c.max_row_nnz > 0 ? c.max_row_nnz : 1;
@@ -672,6 +685,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
     a.vrowA = reinterpret_cast<int32_t*>(p->ws + o_vrowA);
     a.vrowW = reinterpret_cast<int32_t*>(p->ws + o_vrowW);
+    a.thdr = reinterpret_cast<int32_t*>(p->ws + o_thdr);
+    a.task = reinterpret_cast<int32_t*>(p->ws + o_task);
+    a.vtask = reinterpret_cast<int32_t*>(p->ws + o_vtask);
 
     a.desc = reinterpret_cast<int32_t*>(p->ws + o_desc);
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
@@ -702,7 +718,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
     }
     p->grid_fwd = c.batch_size;
-    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.RA, a.RW, a.VCA, a.VCW);
+    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC);
     if (gu >= (1ll << 31)) {
         (void)hipFree(p->ws);
         delete p;
@@ -912,6 +928,8 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     if (count == 0) return RAE_OK;
     hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 3), dim3(RAE_FBT), p->smem_idx, st,
                        p->args, first);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, p->args, first);
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }

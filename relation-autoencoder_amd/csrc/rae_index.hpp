@@ -209,6 +209,44 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     }
 }
 
+// The update's dispatch table of a slot, built once the A and W indexes of the batch exist
+// (a second launch): the update's row waves then find their task with ONE load issued at wave
+// start in parallel with the table header, instead of header -> (class counts) -> segment.
+//   vtask[slot][v]  very heavy rows (A first, then W), v < NVC: one workgroup each
+//   task[slot][t]   wave tasks in dispatch order: very heavy rows beyond NVC, heavy A, heavy W,
+//                   light A, light W (the order the update used to derive from the header)
+//   thdr[slot]      (wave tasks, workgroup tasks, 0, 0)
+// W rows are stored as ~row (negative), A rows as row.
+template <int BT>
+__device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
+    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];
+    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
+    const int HA = hA.z, HW = hW.z, LA = hA.y - hA.z, VA = hA.w, VW = hW.w;
+    const int NV = min(VA + VW, a.NVC), XV = VA + VW - NV;
+    const int T = XV + hA.y + hW.y;
+    int4* vt = reinterpret_cast<int4*>(a.vtask) + slot * a.NVC;
+    int4* tk = reinterpret_cast<int4*>(a.task) + slot * a.TC;
+    const int4* urA = reinterpret_cast<const int4*>(a.urowA) + slot * a.RA;
+    const int4* urW = reinterpret_cast<const int4*>(a.urowW) + slot * a.RW;
+    for (int v = threadIdx.x; v < VA + VW; v += BT) {
+        int4 sg = v < VA ? reinterpret_cast<const int4*>(a.vrowA)[slot * a.VCA + v]
+                         : reinterpret_cast<const int4*>(a.vrowW)[slot * a.VCW + v - VA];
+        if (v >= VA) sg.x = ~sg.x;
+        if (v < NV) vt[v] = sg;
+        else tk[v - NV] = sg;
+    }
+    for (int t = threadIdx.x; t < T - XV; t += BT) {
+        int x = t;
+        int4 sg;
+        if (x < HA) sg = urA[x];
+        else if ((x -= HA) < HW) { sg = urW[x]; sg.x = ~sg.x; }
+        else if ((x -= HW) < LA) sg = urA[a.RA - 1 - x];
+        else { sg = urW[a.RW - 1 - (x - LA)]; sg.x = ~sg.x; }
+        tk[XV + t] = sg;
+    }
+    if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(T, NV, 0, 0);
+}
+
 // Per-example descriptors of the rank's l examples of batch g (slot): everything the forward
 // needs before its W-row gather in ONE coalesced read -- the feature count and CSR start,
 // the NJ entity ids (e1, e2, neg1[t], neg2[t]) and the first dcap feature ids -- instead of

@@ -85,6 +85,11 @@ struct StepArgs {
     int32_t *hdrW, *srecW, *urowW;
     int32_t *vrowA, *vrowW;             // very heavy rows' segments (VCA / VCW per slot)
     int VCA, VCW;
+    // the update's dispatch table per slot (rae_index.hpp build_batch_tasks): every row task in
+    // dispatch order (W rows as ~row), the first NVC very heavy rows as workgroup tasks, and a
+    // header (tasks, workgroup tasks) -- one load away from the wave that runs the task
+    int32_t *thdr, *task, *vtask;
+    int TC, NVC;
     // per-example descriptors of this rank's l examples per slot (rae_index.hpp):
     // [nf, p0, entity ids (NJ), feature ids (<= dcap)], dstride ints each
     int32_t* desc;

@@ -293,11 +293,6 @@ __device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, f
     if (OPT == 0) a.aAb[e] = ac;
 }
 
-__device__ __forceinline__ int4 row_segment(const StepArgs& a, int64_t slot, bool isA, int x) {
-    return isA ? reinterpret_cast<const int4*>(a.urowA)[slot * a.RA + x]    // row, start, end, rec0
-               : reinterpret_cast<const int4*>(a.urowW)[slot * a.RW + x];
-}
-
 template <int OPT, bool V4, int Q, bool XY>
 __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int lane) {
     constexpr int VW = V4 ? 4 : 1;
@@ -329,12 +324,11 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
 // four contiguous chunks, one per wave; wave 0 sums the partial rows in wave order and applies
 // the update (its parameter loads in flight meanwhile).  spart: RAE_NWAVE * 64 * Q vectors.
 template <int OPT, bool V4, int Q, bool XY>
-__device__ void wg_entity_row(const StepArgs& a, int64_t slot, int x, int w, int lane,
+__device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, int lane,
                               typename VecT<V4>::T* spart, float* sgb) {
     constexpr int VW = V4 ? 4 : 1;
     const int r = a.r, nv = r / VW;
     const int64_t base = slot * a.RA;
-    const int4 seg = reinterpret_cast<const int4*>(a.vrowA)[slot * a.VCA + x];
     const int e = seg.x, st = seg.y, en = seg.z;
     const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
     const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
@@ -464,12 +458,11 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
 
 // a very heavy W row per workgroup (as wg_entity_row)
 template <int OPT, bool V4, int Q>
-__device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int x, int w,
+__device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int4 seg, int w,
                                int lane, typename VecT<V4>::T* spart) {
     constexpr int VW = V4 ? 4 : 1;
     const int m = a.m, nv = m / VW;
     const int64_t base = slot * a.RW;
-    const int4 seg = reinterpret_cast<const int4*>(a.vrowW)[slot * a.VCW + x];
     const int f = seg.x, st = seg.y, en = seg.z;
     const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
     const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);

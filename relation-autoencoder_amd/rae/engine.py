@@ -16,6 +16,7 @@ and the update kernels, so every rank applies the identical update.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -147,6 +148,11 @@ class TrainEngine:
         self._index_partitioned = self.L * (2 + 2 * self.s) > 4096 or mbn > 4096
         self._graphs = {}
         self._epoch_mode = None
+        # graph_absolute: every captured step carries its absolute batch index in the launch
+        # (rae_step_*_at: no dependent device-cursor load at kernel start), one graph per
+        # graph_chunk-step chunk of the epoch; otherwise one graph per chunk size, replayed
+        # along the epoch by the device cursor
+        self.graph_absolute = os.environ.get("RAE_GRAPH_ABS", "0") == "1"
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -238,26 +244,49 @@ class TrainEngine:
                        "rae_set_negatives")
             self._epoch_mode = True
 
-    def _steps_eager(self, count, st):
+    def _steps_eager(self, count, st, first=None):
+        """count steps from the device cursor (which then advances past them), or (first
+        given) at absolute batches first, first+1, ... (the cursor is not touched: every
+        cursor-driven run sets it first)."""
         for i in range(count):
-            _lib.check(self.lib.rae_step_forward(self.plan, i, st), "rae_step_forward")
+            if first is None:
+                _lib.check(self.lib.rae_step_forward(self.plan, i, st), "rae_step_forward")
+            else:
+                _lib.check(self.lib.rae_step_forward_at(self.plan, first + i, st),
+                           "rae_step_forward_at")
             if self.exchange is not None:
                 self.exchange(self.exchange_buf)
-            _lib.check(self.lib.rae_step_update(self.plan, i, st), "rae_step_update")
-        _lib.check(self.lib.rae_advance_cursor(self.plan, count, st), "rae_advance_cursor")
+            if first is None:
+                _lib.check(self.lib.rae_step_update(self.plan, i, st), "rae_step_update")
+            else:
+                _lib.check(self.lib.rae_step_update_at(self.plan, first + i, st),
+                           "rae_step_update_at")
+        if first is None:
+            _lib.check(self.lib.rae_advance_cursor(self.plan, count, st), "rae_advance_cursor")
 
-    def _graph(self, count):
-        g = self._graphs.get(count)
+    def _graph(self, count, first=None):
+        key = count if first is None else (int(first), count)
+        g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=s):
-                self._steps_eager(count, self._stream())
+                self._steps_eager(count, self._stream(), first)
             torch.cuda.current_stream(self.device).wait_stream(s)
             _upload_graph(g, s)
-            self._graphs[count] = g
+            self._graphs[key] = g
         return g
+
+    def _chunks(self, first_batch: int, count: int):
+        """(first batch, steps) of every graph run() replays for these batches."""
+        out = []
+        for b, n in self.windows(first_batch, count):
+            full, rem = divmod(n, self.graph_chunk)
+            out += [(b + k * self.graph_chunk, self.graph_chunk) for k in range(full)]
+            if rem:
+                out.append((b + full * self.graph_chunk, rem))
+        return out
 
     def capture(self, count: int | None = None):
         """Capture the HIP graph of ``count`` steps (default: graph_chunk) without running it."""
@@ -288,6 +317,10 @@ class TrainEngine:
         """Capture (without running) every graph run(first_batch, count) will replay, so no
         capture lands inside a timed region."""
         self._ensure_epoch_mode()
+        if self.graph_absolute and self.graph_chunk > 1:
+            for b, n in self._chunks(first_batch, count):
+                self._graph(n, b)
+            return
         for n in sorted(set(self.graph_sizes(first_batch, count))):
             self._graph(n)
 
@@ -310,6 +343,10 @@ class TrainEngine:
                 _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
                 if self._index_partitioned:
                     self.check()
+            if graph and self.graph_chunk > 1 and self.graph_absolute:
+                for cb, cn in self._chunks(b, n):
+                    self._graph(cn, cb).replay()
+                continue
             _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
             if not graph or self.graph_chunk <= 1:
                 self._steps_eager(n, st)
