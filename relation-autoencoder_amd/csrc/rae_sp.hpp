@@ -180,7 +180,11 @@ struct CCache {
         const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
 #pragma unroll
         for (int ra = 0; ra < RA; ++ra) {
+#ifdef RAE_C_HOT
+            const int i = (gid + RAE_NG * ra) & 7;   // diagnostic: 8 hot rows (L1 hits)
+#else
             const int i = min(r0 + gid + RAE_NG * ra, Dm.r - 1);
+#endif
 #pragma unroll
             for (int cc = 0; cc < CC; ++cc) {
                 const int c = min(c0 + q + 16 * cc, mv - 1);
@@ -724,7 +728,11 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         for (int k = 0; k < KF; ++k) {
             const int f = slot + NSL * k;
             const bool ok = slot < NSL && f < nf;
+#ifdef RAE_W_ROW0
+            const int fi = 0;                  // diagnostic: every W row from row 0 (cache hits)
+#else
             const int fi = S.sfidx[f < 256 ? f : 255];
+#endif
             wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
             fv[k] = ok ? S.sfval[f < 256 ? f : 255] : 0.f;
         }

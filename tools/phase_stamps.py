@@ -134,7 +134,8 @@ def main():
         ex = f[HA + HW:gf]
         clk += list((ex[:, 15] - ex[:, 14]) * 100.0 / ((ex[:, 7] - ex[:, 0]) * 100.0) * 100.0 / 100.0)
     print(f"  example-WG shader clock (s_memtime ticks / s_memrealtime): median {np.median(clk) * 100:.0f} MHz")
-    tnames = ["C-tile", "R-tile", "Wb-tile", "cost", "A-row", "W-row", "A-heavy", "W-heavy"]
+    tnames = ["C-tile", "R-tile", "Wb-tile", "cost", "A-row", "W-row", "A-heavy", "W-heavy",
+              "A-vheavy", "W-vheavy"]
     allw = np.concatenate(up)
     valid = allw[:, 0] > 0
     allw = allw[valid]
@@ -146,18 +147,21 @@ def main():
     for ty, nm in enumerate(tnames):
         d = []
         st_ = []
+        en_ = []
         for t0, t1, v in t0s:
             sel = v[v[:, 1] == ty]
             d += list((sel[:, 2] - sel[:, 0]) / 100.0)
             st_ += list((sel[:, 0] - t0) / 100.0)
+            en_ += list((sel[:, 2] - t0) / 100.0)
         if d:
             extra = ""
-            if ty >= 4:
+            if ty >= 4 and ty < 8:
                 sg = np.concatenate([(v[v[:, 1] == ty][:, 3] - v[v[:, 1] == ty][:, 0]) / 100.0
                                      for _, _, v in t0s])
                 extra = f"  (start->segment {np.median(sg):.2f}, segment->end {np.median(d) - np.median(sg):.2f})"
             print(f"    {nm:8s} n={len(d) // len(t0s):5d}  busy {np.median(d):.2f}/{np.max(d):.2f}"
-                  f"  start {np.median(st_):.2f}/{np.max(st_):.2f}{extra}")
+                  f"  start {np.median(st_):.2f}/{np.max(st_):.2f}  end p50 {np.median(en_):.2f}"
+                  f" p99 {np.percentile(en_, 99):.2f} max {np.max(en_):.2f}{extra}")
     mids = []
     for t0, t1, v in t0s:
         sel = v[(v[:, 1] == 0) & (v[:, 3] > 0)]
