@@ -664,6 +664,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     if (splitenv && (splitenv[0] == '0' || splitenv[0] == '1')) p->sp_split = !bil && splitenv[0] == '1';
     const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
     a.Lp = (L + 31) / 32 * 32;
+    {
+        const char* fp = getenv("RAE_FUSEPREP");     // A/B override: 0 keeps k_bil_prep
+        a.fuse_prep = (a.bf16 && c.world_size == 1 && !(fp && fp[0] == '0')) ? 1 : 0;
+    }
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
@@ -869,7 +873,7 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         // branch (123 vs 112 us/step: the cross-stream graph edges cost more than the overlap);
         // k_bil_rows with all P fragments in LDS and every load of a tile hoisted into one round
         // trip (29 vs 24 us: two workgroups per CU and the per-workgroup staging cost more).
-        if (a.bf16) {
+        if (a.bf16 && !a.fuse_prep) {
             const int gp = 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
             RAE_LAUNCH(p, k_bil_prep, dim3(gp), bt, 0, st, a);
         }

@@ -39,11 +39,27 @@ namespace rae {
 
 typedef float rae_bf4 __attribute__((ext_vector_type(4)));
 #define RAE_IB 8     // i rows per dP partial block (k_bil_dp)
+#ifndef RAE_RT_PAIR
+#define RAE_RT_PAIR 1      // R-gradient: two K-steps' operand loads per round trip
+#endif
+#ifndef RAE_RT_STAGGER
+#define RAE_RT_STAGGER 1   // k_bil_rows: odd workgroups compute before issuing their tile reads
+#endif
 #ifndef RAE_KG
 #define RAE_KG 8     // 16-column tiles of m per pass of one R-row task (task_bilinear_rows)
 #endif
 
 // ---- k_bil_enc: encoder + hybrid SP projections --------------------------------------------
+
+// P[b][k] of example b as its element of the bf16 B fragments k_bil_rows reads (k_bil_prep's
+// pfrag layout: fragment (b / 32, k / 16), lane 16 ((b % 32) / 8) + k % 16, element b % 8)
+__device__ __forceinline__ void prep_p_fragment(const StepArgs& a, int b, int k, float p) {
+    const int nkt = (a.m + 15) / 16, bb = b & 31;
+    const int64_t t = (int64_t)(b >> 5) * nkt + (k >> 4);
+    const int lane = 16 * (bb >> 3) + (k & 15);
+    reinterpret_cast<__bf16*>(a.pfrag)[(t * 64 + lane) * 8 + (bb & 7)] = (__bf16)p;
+}
+
 template <bool V4>
 __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
     const DynDims Dm(a);
@@ -65,14 +81,20 @@ __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
     for (int k = threadIdx.x; k < m; k += RAE_FBT) {
         rec[a.lay.oP + k] = S.sP[k];
         rec[a.lay.oZ + k] = S.sZ[k];
+        if (a.fuse_prep) prep_p_fragment(a, bg, k, S.sP[k]);
     }
     const float* A1 = a.A + (int64_t)S.sids[0] * r;
     const float* A2 = a.A + (int64_t)S.sids[1] * r;
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        rec[a.lay.oA1 + i] = A1[i];
-        rec[a.lay.oA2 + i] = A2[i];
+        const float v1 = A1[i], v2 = A2[i];
+        rec[a.lay.oA1 + i] = v1;
+        rec[a.lay.oA2 + i] = v2;
         rec[a.lay.oV1 + i] = hybrid ? S.swC1[i] : 0.f;
         rec[a.lay.oV2 + i] = hybrid ? S.swC2[i] : 0.f;
+        if (a.fuse_prep) {
+            a.facT[((int64_t)1 * r + i) * a.Lp + bg] = v1;
+            a.facT[((int64_t)2 * r + i) * a.Lp + bg] = v2;
+        }
     }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];     // H until k_bil_dec
 }
@@ -791,8 +813,13 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
                 n1 += S.coef[3 * (2 + t)] * S.rows[t * r4 + i];
                 n2 += S.coef[3 * (2 + s + t) + 1] * S.rows[(s + t) * r4 + i];
             }
-            rec[a.lay.oX + i] = dOne * S.a1[i] + n1;
+            const float xv = dOne * S.a1[i] + n1;
+            rec[a.lay.oX + i] = xv;
             rec[a.lay.oY + i] = n2;
+            if (a.fuse_prep) {
+                a.facT[(int64_t)i * a.Lp + bg] = xv;
+                a.facT[((int64_t)3 * r + i) * a.Lp + bg] = n2;
+            }
             rec[a.lay.odw1 + i] = hybrid ? ca1 * S.a1[i] + n1 : 0.f;
             rec[a.lay.odw2 + i] = hybrid ? ca2 * S.a2[i] + n2 : 0.f;
         }
@@ -993,36 +1020,64 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     const float* a1t = a.facT + (int64_t)(r + i) * Lp;
     const float* a2t = a.facT + (int64_t)(2 * r + j) * Lp;
     const float* yt = a.facT + (int64_t)(3 * r + j) * Lp;
-    for (int b0 = 0; b0 < L; b0 += 32) {
-        const int bb = b0 + 8 * g;
+    // one K-step (32 examples): the lane's 8 examples of each factor and the P fragments
+    struct Step {
         float xv[8], a1v[8], a2v[8], yv[8];
-        *reinterpret_cast<float4*>(xv) = *reinterpret_cast<const float4*>(xt + bb);
-        *reinterpret_cast<float4*>(xv + 4) = *reinterpret_cast<const float4*>(xt + bb + 4);
-        *reinterpret_cast<float4*>(a1v) = *reinterpret_cast<const float4*>(a1t + bb);
-        *reinterpret_cast<float4*>(a1v + 4) = *reinterpret_cast<const float4*>(a1t + bb + 4);
-        *reinterpret_cast<float4*>(a2v) = *reinterpret_cast<const float4*>(a2t + bb);
-        *reinterpret_cast<float4*>(a2v + 4) = *reinterpret_cast<const float4*>(a2t + bb + 4);
-        *reinterpret_cast<float4*>(yv) = *reinterpret_cast<const float4*>(yt + bb);
-        *reinterpret_cast<float4*>(yv + 4) = *reinterpret_cast<const float4*>(yt + bb + 4);
         rae_bf16x8 pb[RAE_KG];
+    };
+    auto load = [&](Step& st, int b0) {
+        const int bb = b0 + 8 * g;
+        *reinterpret_cast<float4*>(st.xv) = *reinterpret_cast<const float4*>(xt + bb);
+        *reinterpret_cast<float4*>(st.xv + 4) = *reinterpret_cast<const float4*>(xt + bb + 4);
+        *reinterpret_cast<float4*>(st.a1v) = *reinterpret_cast<const float4*>(a1t + bb);
+        *reinterpret_cast<float4*>(st.a1v + 4) = *reinterpret_cast<const float4*>(a1t + bb + 4);
+        *reinterpret_cast<float4*>(st.a2v) = *reinterpret_cast<const float4*>(a2t + bb);
+        *reinterpret_cast<float4*>(st.a2v + 4) = *reinterpret_cast<const float4*>(a2t + bb + 4);
+        *reinterpret_cast<float4*>(st.yv) = *reinterpret_cast<const float4*>(yt + bb);
+        *reinterpret_cast<float4*>(st.yv + 4) = *reinterpret_cast<const float4*>(yt + bb + 4);
         const uint4* pf = a.pfrag + ((int64_t)(b0 / 32) * nkt + kg0) * 64 + lane;
 #pragma unroll
         for (int q = 0; q < RAE_KG; ++q) {
             const uint4 u = pf[(q < nk ? q : 0) * 64];
-            pb[q] = *reinterpret_cast<const rae_bf16x8*>(&u);
+            st.pb[q] = *reinterpret_cast<const rae_bf16x8*>(&u);
         }
+    };
+    auto mfma = [&](const Step& st) {
         rae_bf16x8 ua;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const float u = xv[e] * a2v[e] + a1v[e] * yv[e];    // zero past L (padded factors)
+            const float u = st.xv[e] * st.a2v[e] + st.a1v[e] * st.yv[e];   // zero past L (padded)
             ua[e] = (__bf16)(ijv ? u : 0.f);
         }
 #pragma unroll
         for (int q = 0; q < RAE_KG; ++q) {          // D[k][ij]: P^T as A, U as B
             if (q >= nk) continue;
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pb[q], ua, acc[q], 0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st.pb[q], ua, acc[q], 0, 0, 0);
         }
+    };
+#if RAE_RT_PAIR
+    // two K-steps' loads issued before either step's MFMAs: half the dependent round trips
+    int b0 = 0;
+    for (; b0 + 32 < L; b0 += 64) {
+        Step s0, s1;
+        load(s0, b0);
+        load(s1, b0 + 32);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma(s0);
+        mfma(s1);
     }
+    if (b0 < L) {
+        Step s0;
+        load(s0, b0);
+        mfma(s0);
+    }
+#else
+    for (int b0 = 0; b0 < L; b0 += 32) {
+        Step s0;
+        load(s0, b0);
+        mfma(s0);
+    }
+#endif
 }
 
 // One wave: 16 rows ij x all m columns.  The gradient tile comes out transposed (D[k][ij]:
@@ -1148,6 +1203,14 @@ __device__ void task_bilinear_rows_lds(const StepArgs& a, int ijt, int slot, int
     const int nv = nrow * m / 4;                          // float4s of the tile
     float* sR = sw;
     float* sA = sw + 16 * m;
+    rae_bf4 acc[RAE_KG];
+#pragma unroll
+    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+    const int nk = (m + 15) / 16;                         // <= RAE_KG: one column group
+    // RAE_RT_STAGGER: every other workgroup runs its gradient before its tile reads are issued,
+    // so half of the launch's read-modify-write traffic meets the other half's gradient phase
+    const bool pre = RAE_RT_STAGGER && (blockIdx.x & 1);
+    if (pre) bilinear_rows_acc_bf16(a, ijt, 0, nk, acc, lane);
     for (int n = 0; n * 64 < nv; ++n) {
         const int idx = n * 64 + lane;
         if (idx < nv) {
@@ -1160,11 +1223,7 @@ __device__ void task_bilinear_rows_lds(const StepArgs& a, int ijt, int slot, int
     }
     const bool reg = a.reg_on && a.ext_reg;
     float l1 = 0.f, l2 = 0.f;
-    rae_bf4 acc[RAE_KG];
-#pragma unroll
-    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-    const int nk = (m + 15) / 16;                         // <= RAE_KG: one column group
-    bilinear_rows_acc_bf16(a, ijt, 0, nk, acc, lane);
+    if (!pre) bilinear_rows_acc_bf16(a, ijt, 0, nk, acc, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the tile has landed in LDS
 #pragma unroll
     for (int q = 0; q < RAE_KG; ++q) {

@@ -114,6 +114,8 @@ struct StepArgs {
     float* facT;
     uint4* pfrag;
     int Lp;
+    int fuse_prep;       // single rank: the forward kernels write facT / pfrag themselves (no
+                         // k_bil_prep launch); padding (b >= L, k >= m) stays zero from creation
     double* regpart;     // [nreg][2] L1/L2 partials of regularised rows
     int nregC;           // number of decoder-row partial slots
     int nregW;           // number of dense-W block partial slots
