@@ -8,6 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 bash tools/gpu_r2.sh $TAG || exit 1
 bash tools/gpu_pmc2.sh $TAG/pmc c3 || exit 1
+BX="--batch-size 800 --no-label-pass" bash tools/gpu_pmc2.sh $TAG/pmc800 c3 || exit 1
 cd $R
 for C in c2 c5 c4; do
   timeout -k 10 400 python3 -u bench.py --config $C --no-cpu-baseline --no-label-pass --steps 256 --warmup 32 > $O/bench_$C.json 2> $O/bench_$C.err || { echo bench $C failed; tail -20 $O/bench_$C.err; exit 1; }

@@ -29,9 +29,12 @@ def _rows(d):
 def _group(name):
     n = name.split("(")[0].replace("void ", "").strip()
     base = n.split("<")[0]
-    if base == "k_forward" or base in ("k_bil_enc", "k_bil_m", "k_bil_dec", "k_bil_dp", "k_bil_fin"):
+    if base == "k_forward" or base in ("k_bil_enc", "k_bil_mt", "k_bil_dec", "k_bil_dp", "k_bil_dp2",
+                                       "k_bil_fin", "k_sp_enc", "k_sp_cp", "k_sp_dec", "k_sp_ctdw",
+                                       "k_sp_fin"):
         return "k_forward", base
-    if base in ("k_update", "k_update_bil", "k_dense_w", "k_finalize_cost"):
+    if base in ("k_update", "k_update_bil", "k_bil_prep", "k_bil_rows", "k_dense_w",
+                "k_finalize_cost"):
         return "k_update", base
     return None, base
 
@@ -56,7 +59,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--out", default=None)
-    args = ap.parse_args()
+    args, extra = ap.parse_known_args()      # extra: the bench.py arguments of the passes
     fe = collect(args.fetch_dir, "FETCH_SIZE")
     wr = collect(args.write_dir, "WRITE_SIZE")
     per_kernel = {}
@@ -69,7 +72,7 @@ def main():
                             "launches": nf,
                             "traffic_bytes": 2.0 * 1024.0 * f / nf + 1024.0 * w / nw}
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py "
-                     f"--config {args.config}; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch",
+                     f"--config {args.config} {' '.join(extra)}; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch",
            "per_kernel": per_kernel}
     groups = defaultdict(float)
     for base, v in per_kernel.items():
