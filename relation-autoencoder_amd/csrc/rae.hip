@@ -177,8 +177,11 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_SPLIT_RM
 #define RAE_SPLIT_RM 32768    // r*m above which the SP forward runs split (rae_sp_split.hpp)
 #endif
+#ifndef RAE_NVC_DIV
+#define RAE_NVC_DIV 2         // very heavy row workgroup slots: max(32, L / RAE_NVC_DIV)
+#endif
 #ifndef RAE_UPD_WGCAP
-#define RAE_UPD_WGCAP 1536    // row-task workgroups: 6 per CU (24 waves) on 256 CUs
+#define RAE_UPD_WGCAP 6144    // row-task workgroups (grid-stride beyond; 1536 = one resident round)
 #endif
 __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
@@ -618,10 +621,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.VCW = a.RW / (RAE_VHEAVY + 1) + 1;
     const size_t o_vrowA = take(16ull * W_ * a.VCA), o_vrowW = take(16ull * W_ * a.VCW);
     // the update's dispatch table: every unique row is at most one task (TC = records), and
-    // NVC very heavy rows get a workgroup each (L/8 at least 32 -- the rest run as wave tasks)
+    // NVC very heavy rows get a workgroup each (L / RAE_NVC_DIV, at least 32 -- the rest run as
+    // wave tasks)
     a.TC = a.RA + a.RW;
     {
-        const int nvc = L / 8 > 32 ? L / 8 : 32;
+        const int nvc = L / RAE_NVC_DIV > 32 ? L / RAE_NVC_DIV : 32;
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
     }
     const size_t o_thdr = take(16 * W_), o_task = take(16ull * W_ * a.TC);
