@@ -177,6 +177,12 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_SPLIT_RM
 #define RAE_SPLIT_RM 32768    // r*m above which the SP forward runs split (rae_sp_split.hpp)
 #endif
+#ifndef RAE_ROWPCT
+#define RAE_ROWPCT 100        // row-task waves per 100 dispatch-table capacity entries
+#endif
+#ifndef RAE_NVC_MIN
+#define RAE_NVC_MIN 32
+#endif
 #ifndef RAE_NVC_DIV
 #define RAE_NVC_DIV 2         // very heavy row workgroup slots: max(32, L / RAE_NVC_DIV)
 #endif
@@ -186,7 +192,7 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
     const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
-    int64_t rows = ((int64_t)TC + RAE_NWAVE - 1) / RAE_NWAVE;
+    int64_t rows = ((int64_t)TC * RAE_ROWPCT / 100 + RAE_NWAVE - 1) / RAE_NWAVE;
     if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
     return (int64_t)nT + nP + NVC + rows;
 }
@@ -625,7 +631,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // wave tasks)
     a.TC = a.RA + a.RW;
     {
-        const int nvc = L / RAE_NVC_DIV > 32 ? L / RAE_NVC_DIV : 32;
+        const int nvc = L / RAE_NVC_DIV > RAE_NVC_MIN ? L / RAE_NVC_DIV : RAE_NVC_MIN;
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
     }
     const size_t o_thdr = take(16 * W_), o_task = take(16ull * W_ * a.TC);

@@ -580,6 +580,38 @@ def test_hot_rows_vs_oracle(built_lib, cuda_dev, dec):
     _assert_params_close(_params(ind), tr.params, "hot")
 
 
+@pytest.mark.parametrize("dec", ["sp", "rescal+sp"])
+def test_very_heavy_rows_beyond_workgroup_slots(built_lib, cuda_dev, dec):
+    """More very heavy rows (> 16 records per step) than the update has workgroup slots for
+    (NVC = max(32, L/2) = 32 at L = 64): the dispatch table hands the excess to single waves
+    (rae_index.hpp build_batch_tasks).  60 entities and 40 features under a 64-example batch
+    give ~23 records per entity and ~22 per feature: ~90 very heavy rows per step."""
+    from rae.data import DatasetManager
+    from rae.inducer import ReconstructInducer
+    g = np.random.RandomState(5)
+    N, d, n = 640, 40, 60
+    lens = g.randint(10, 18, size=N)
+    rows = np.repeat(np.arange(N), lens)
+    cols = np.concatenate([g.choice(d, size=k, replace=False) for k in lens])
+    X = sp.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(N, d))
+    a1 = g.randint(0, n, N).astype(np.int32)
+    a2 = g.randint(0, n, N).astype(np.int32)
+    a1[:n] = np.arange(n)
+    data = DatasetManager.from_arrays(X, a1, a2, n_entities=n)
+    m, r, s, l, ep = 8, 16, 10, 64, 2
+    # the W rows alone already exceed the 32 workgroup slots in every batch
+    vh_w = [int((np.bincount(cols[rows_b], minlength=d) > 16).sum())
+            for rows_b in (np.isin(rows, np.arange(b * l, (b + 1) * l)) for b in range(N // l))]
+    assert min(vh_w) > 32, vh_w
+    ind = ReconstructInducer(data, {"train": {}}, np.random.RandomState(2), ep, 0.1, l, r, m, s,
+                             0.0, 0.0, "adagrad", "vheavy", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=4)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "vheavy")
+
+
 def test_initialize_then_train_restarts_like_reference(built_lib, cuda_dev):
     """test.py:33-46's sequence: train(), initialize(), train().  The second train() runs all
     its epochs again from epoch 0 with a fresh zero-accumulator optimizer
