@@ -291,6 +291,7 @@ def main():
     n_it = min(args.kernel_iters, nb - b0, eng.index_window)
     lib.rae_build_index(plan, b0, n_it, sp_)
     lib.rae_set_cursor(plan, b0, sp_)
+    eng.cursor_moved()
 
     def _ev():
         h = C.c_void_p()

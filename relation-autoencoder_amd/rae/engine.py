@@ -153,6 +153,10 @@ class TrainEngine:
         # graph_chunk-step chunk of the epoch; otherwise one graph per chunk size, replayed
         # along the epoch by the device cursor
         self.graph_absolute = os.environ.get("RAE_GRAPH_ABS", "0") == "1"
+        # batch the device cursor holds after this engine's last cursor-driven run (None:
+        # unknown -- someone else drove it); run() skips its rae_set_cursor launch when the
+        # cursor already points at the requested batch (consecutive runs of an epoch)
+        self._cursor_at = None
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -169,6 +173,11 @@ class TrainEngine:
             self.close()
         except Exception:
             pass
+
+    def cursor_moved(self):
+        """Tell the engine the device cursor was driven outside run() (direct rae_set_cursor /
+        rae_step_* calls on its plan): the next run() sets it again."""
+        self._cursor_at = None
 
     def check(self):
         _lib.check(self.lib.rae_check(self.plan), "rae_check")
@@ -347,7 +356,9 @@ class TrainEngine:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
                 continue
-            _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
+            if self._cursor_at != b or os.environ.get("RAE_CURSOR_RESET") == "1":
+                _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
+            self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
                 self._steps_eager(n, st)
             else:
@@ -358,6 +369,7 @@ class TrainEngine:
                         g.replay()
                 if rem:
                     self._graph(rem).replay()
+            self._cursor_at = b + n
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):
