@@ -177,6 +177,9 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_SPLIT_RM
 #define RAE_SPLIT_RM 32768    // r*m above which the SP forward runs split (rae_sp_split.hpp)
 #endif
+#ifndef RAE_ROWS_FIRST
+#define RAE_ROWS_FIRST 0      // update: dispatch the row tasks ahead of the dense tiles
+#endif
 #ifndef RAE_ROWPCT
 #define RAE_ROWPCT 100        // row-task waves per 100 dispatch-table capacity entries
 #endif
@@ -210,8 +213,8 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     // record offset derived from them is then scalar (s_load of the segment, SGPR soffsets,
     // scalar branches) instead of VGPR-resident and exec-masked
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
-    const int gw = wg * RAE_NWAVE + w;
+    const int wgp = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    const int gw = wgp * RAE_NWAVE + w;
     const int64_t g = step_batch(a);
     const int64_t ex0 = g * (int64_t)a.L;
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
@@ -219,6 +222,13 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     const int nT = nCt + mt;
     const int nPt = update_wave_free_tasks(a.dec, a.r, a.m);
     const int nP = (nPt + RAE_NWAVE - 1) / RAE_NWAVE;
+    // logical task order: tiles, cost, very heavy rows, row waves; RAE_ROWS_FIRST dispatches the
+    // row part first (physical order: very heavy rows, row waves, tiles, cost)
+    int wg = wgp;
+    if (RAE_ROWS_FIRST) {
+        const int nrow = (int)gridDim.x - nT - nP;
+        wg = wgp < nrow ? nT + nP + wgp : wgp - nrow;
+    }
     const int64_t slot = g % a.index_window;
 #ifdef RAE_STAMPS
     unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
