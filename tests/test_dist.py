@@ -1,9 +1,9 @@
-"""Data-parallel path with world_size 2 and 4, one process per rank, launched the
+"""Data-parallel path with world_size 2, 4 and 8, one process per rank, launched the
 way bench.py is launched for N > 1 (torch.distributed.run, 127.0.0.1).
 
 CPU (gloo): the exchange all-gather, and the row/negative-column partition + global loss
 normaliser on the float64 oracle == the single-process oracle at the global batch.
-GPU: the HIP path itself with two / four ranks on one GPU (gloo, host-staged exchange) == the
+GPU: the HIP path itself with two / four / eight ranks on one GPU (gloo, host-staged exchange) == the
 oracle at the global batch, and all replicas bit-identical.
 """
 import os
@@ -57,7 +57,8 @@ def test_exchange_all_gather_gloo(tmp_path):
 
 @pytest.mark.parametrize("decoder,lambda1,ws", [("sp", 0.0, 2), ("rescal", 0.0, 2),
                                                 ("rescal+sp", 0.0, 2), ("sp", 0.01, 2),
-                                                ("sp", 0.0, 4), ("rescal+sp", 0.01, 4)])
+                                                ("sp", 0.0, 4), ("rescal+sp", 0.01, 4),
+                                                ("sp", 0.0, 8)])
 def test_partition_equals_global_batch(tmp_path, decoder, lambda1, ws):
     _launch(["oracle", str(tmp_path), decoder, str(lambda1)], nproc=ws)
     tr, costs = _single_process_oracle(decoder, lambda1, ws)
@@ -70,7 +71,8 @@ def test_partition_equals_global_batch(tmp_path, decoder, lambda1, ws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4)])
+@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4),
+                                        ("sp", 8), ("rescal+sp", 8)])
 def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws):
     _launch(["gpu", str(tmp_path), decoder], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
