@@ -39,6 +39,9 @@ namespace rae {
 
 typedef float rae_bf4 __attribute__((ext_vector_type(4)));
 #define RAE_IB 8     // i rows per dP partial block (k_bil_dp)
+#ifndef RAE_FAC_BF16
+#define RAE_FAC_BF16 1     // R-gradient factor copies (facT) stored as bf16: half the operand loads
+#endif
 #ifndef RAE_RT_PAIR
 #define RAE_RT_PAIR 1      // R-gradient: two K-steps' operand loads per round trip
 #endif
@@ -50,6 +53,14 @@ typedef float rae_bf4 __attribute__((ext_vector_type(4)));
 #endif
 
 // ---- k_bil_enc: encoder + hybrid SP projections --------------------------------------------
+
+// factor f (0 X, 1 A1, 2 A2, 3 Y) of example b at row i of the transposed operand copy k_bil_rows
+// reads (RAE_FAC_BF16: stored as bf16, the precision the R-gradient MFMA consumes it at)
+__device__ __forceinline__ void put_fac(const StepArgs& a, int f, int i, int b, float v) {
+    const int64_t o = ((int64_t)f * a.r + i) * a.Lp + b;
+    if (RAE_FAC_BF16) reinterpret_cast<__bf16*>(a.facT)[o] = (__bf16)v;
+    else a.facT[o] = v;
+}
 
 // P[b][k] of example b as its element of the bf16 B fragments k_bil_rows reads (k_bil_prep's
 // pfrag layout: fragment (b / 32, k / 16), lane 16 ((b % 32) / 8) + k % 16, element b % 8)
@@ -92,8 +103,8 @@ __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
         rec[a.lay.oV1 + i] = hybrid ? S.swC1[i] : 0.f;
         rec[a.lay.oV2 + i] = hybrid ? S.swC2[i] : 0.f;
         if (a.fuse_prep) {
-            a.facT[((int64_t)1 * r + i) * a.Lp + bg] = v1;
-            a.facT[((int64_t)2 * r + i) * a.Lp + bg] = v2;
+            put_fac(a, 1, i, bg, v1);
+            put_fac(a, 2, i, bg, v2);
         }
     }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];     // H until k_bil_dec
@@ -817,8 +828,8 @@ __device__ void bil_decode(const StepArgs& a, int64_t g, int bl, char* smem) {
             rec[a.lay.oX + i] = xv;
             rec[a.lay.oY + i] = n2;
             if (a.fuse_prep) {
-                a.facT[(int64_t)i * a.Lp + bg] = xv;
-                a.facT[((int64_t)3 * r + i) * a.Lp + bg] = n2;
+                put_fac(a, 0, i, bg, xv);
+                put_fac(a, 3, i, bg, n2);
             }
             rec[a.lay.odw1 + i] = hybrid ? ca1 * S.a1[i] + n1 : 0.f;
             rec[a.lay.odw2 + i] = hybrid ? ca2 * S.a2[i] + n2 : 0.f;
@@ -984,7 +995,7 @@ __device__ void bil_prep(const StepArgs& a) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int ii = (tid >> 5) + 8 * u, bb = tid & 31, i = it * 64 + ii;
-            if (i < r) a.facT[((int64_t)f * r + i) * Lp + bs * 32 + bb] = tile[bb][ii];
+            if (i < r) put_fac(a, f, i, bs * 32 + bb, tile[bb][ii]);
         }
     } else if (blk < nfacb + nbs * nkt) {
         const int t = blk - nfacb, bs = t / nkt, kt = t - bs * nkt;
@@ -1020,6 +1031,11 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     const float* a1t = a.facT + (int64_t)(r + i) * Lp;
     const float* a2t = a.facT + (int64_t)(2 * r + j) * Lp;
     const float* yt = a.facT + (int64_t)(3 * r + j) * Lp;
+    const __bf16* fb = reinterpret_cast<const __bf16*>(a.facT);
+    const __bf16* xb = fb + (int64_t)i * Lp;
+    const __bf16* a1b = fb + (int64_t)(r + i) * Lp;
+    const __bf16* a2b = fb + (int64_t)(2 * r + j) * Lp;
+    const __bf16* yb = fb + (int64_t)(3 * r + j) * Lp;
     // one K-step (32 examples): the lane's 8 examples of each factor and the P fragments
     struct Step {
         float xv[8], a1v[8], a2v[8], yv[8];
@@ -1027,6 +1043,19 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     };
     auto load = [&](Step& st, int b0) {
         const int bb = b0 + 8 * g;
+        if (RAE_FAC_BF16) {                              // 8 examples of a factor: one 16-B load
+            const rae_bf16x8 vx = *reinterpret_cast<const rae_bf16x8*>(xb + bb);
+            const rae_bf16x8 v1 = *reinterpret_cast<const rae_bf16x8*>(a1b + bb);
+            const rae_bf16x8 v2 = *reinterpret_cast<const rae_bf16x8*>(a2b + bb);
+            const rae_bf16x8 vy = *reinterpret_cast<const rae_bf16x8*>(yb + bb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                st.xv[e] = (float)vx[e];
+                st.a1v[e] = (float)v1[e];
+                st.a2v[e] = (float)v2[e];
+                st.yv[e] = (float)vy[e];
+            }
+        } else {
         *reinterpret_cast<float4*>(st.xv) = *reinterpret_cast<const float4*>(xt + bb);
         *reinterpret_cast<float4*>(st.xv + 4) = *reinterpret_cast<const float4*>(xt + bb + 4);
         *reinterpret_cast<float4*>(st.a1v) = *reinterpret_cast<const float4*>(a1t + bb);
@@ -1035,6 +1064,7 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
         *reinterpret_cast<float4*>(st.a2v + 4) = *reinterpret_cast<const float4*>(a2t + bb + 4);
         *reinterpret_cast<float4*>(st.yv) = *reinterpret_cast<const float4*>(yt + bb);
         *reinterpret_cast<float4*>(st.yv + 4) = *reinterpret_cast<const float4*>(yt + bb + 4);
+        }
         const uint4* pf = a.pfrag + ((int64_t)(b0 / 32) * nkt + kg0) * 64 + lane;
 #pragma unroll
         for (int q = 0; q < RAE_KG; ++q) {
