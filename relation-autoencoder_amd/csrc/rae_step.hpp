@@ -109,7 +109,7 @@ struct StepArgs {
     int nib;             // bilinear: number of i-blocks of the dP contraction
     int bf16;            // bilinear: bf16 MFMA operands (fp32 accumulation) for the R GEMMs
     // bf16 R-gradient operands laid out by k_bil_prep after the exchange: the rank-2 factors
-    // X, A1, A2, Y of the global batch transposed to (4, r, Lp) fp32 (example-minor, Lp = L
+    // X, A1, A2, Y of the global batch transposed to (4, r, Lp) bf16 (RAE_FAC_BF16; example-minor, Lp = L
     // rounded up to 32, zero padded) and P as ready B fragments (L/32, K/16, 64 lanes) x 8 bf16
     float* facT;
     uint4* pfrag;
