@@ -349,6 +349,44 @@ def test_cursor_and_absolute_batch_launches_agree(built_lib, cuda_dev):
     assert np.array_equal(out[0][1], out[1][1])
 
 
+def test_consecutive_runs_skip_cursor_reset(built_lib, cuda_dev):
+    """engine.run() skips its rae_set_cursor launch when the device cursor already points at the
+    requested batch (bench.py's warm-up -> timed region): split runs, an explicit cursor move in
+    between and one whole run all train bit-identically."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    out = []
+    for mode in ("whole", "split", "moved"):
+        data, gold = synthetic_dataset(1200, 900, 5, seed=13)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 40, 24, 12, 5,
+                                 0.0, 0.0, "adagrad", "cur", "sp", False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=4)
+        ind.compile_function()
+        eng = ind.engine
+        n1, n2 = ind.draw_epoch_negatives()
+        eng.set_epoch_negatives(n1, n2)
+        nb = eng.nb
+        if mode == "whole":
+            eng.run(0, nb)
+        else:
+            eng.run(0, 5)
+            if mode == "moved":                     # someone else drove the cursor meanwhile
+                import ctypes as C
+                import torch
+                st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+                assert eng.lib.rae_set_cursor(eng.plan, 17, st) == 0
+                eng.cursor_moved()
+            eng.run(5, nb - 5)
+        import torch
+        torch.cuda.synchronize()
+        eng.check()
+        out.append((_params(ind), eng.costs[:nb].cpu().numpy().copy()))
+    for o in out[1:]:
+        for k in out[0][0]:
+            assert np.array_equal(out[0][0][k], o[0][k]), k
+        assert np.array_equal(out[0][1], o[1])
+
+
 @pytest.mark.parametrize("shape", [(100, 200, 20, 100), (60, 96, 5, 40)], ids=["c5", "padded"])
 @pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
 def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
