@@ -183,6 +183,10 @@ def cpu_baseline(data, cfg, l, budget_s):
                 ms_per_step=1e3 * l / best["value"])
 
 
+# A/B override: RAE_LAST_ADVANCE=1 keeps the cursor advance in the timed run's last graph
+LAST_ADV = os.environ.get("RAE_LAST_ADVANCE") == "1"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,7 +250,7 @@ def main():
     try:
         if graphed:                        # capture every graph the warm-up and the timed
             eng.capture_for(0, W)          # steps replay before running either (no capture
-            eng.capture_for(W, K)          # inside the timed region)
+            eng.capture_for(W, K, last_advance=LAST_ADV)   # inside the timed region)
         eng.run(0, W, index=not prebuilt)
     except RuntimeError as e:              # e.g. a collective the runtime cannot capture
         if ws == 1 or not graphed:
@@ -262,7 +266,8 @@ def main():
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    eng.run(W, K, index=not prebuilt)
+    # no run follows the timed one on this cursor: its last graph skips the cursor advance
+    eng.run(W, K, index=not prebuilt, last_advance=LAST_ADV)
     torch.cuda.synchronize()
     rdist.barrier()
     torch.cuda.synchronize()

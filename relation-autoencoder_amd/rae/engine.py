@@ -253,8 +253,9 @@ class TrainEngine:
                        "rae_set_negatives")
             self._epoch_mode = True
 
-    def _steps_eager(self, count, st, first=None):
-        """count steps from the device cursor (which then advances past them), or (first
+    def _steps_eager(self, count, st, first=None, advance=True):
+        """count steps from the device cursor (which then advances past them unless
+        advance=False: a run's last graph, whose successor sets the cursor anyway), or (first
         given) at absolute batches first, first+1, ... (the cursor is not touched: every
         cursor-driven run sets it first)."""
         for i in range(count):
@@ -270,18 +271,18 @@ class TrainEngine:
             else:
                 _lib.check(self.lib.rae_step_update_at(self.plan, first + i, st),
                            "rae_step_update_at")
-        if first is None:
+        if first is None and advance:
             _lib.check(self.lib.rae_advance_cursor(self.plan, count, st), "rae_advance_cursor")
 
-    def _graph(self, count, first=None):
-        key = count if first is None else (int(first), count)
+    def _graph(self, count, first=None, advance=True):
+        key = (count if advance else ("last", count)) if first is None else (int(first), count)
         g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=s):
-                self._steps_eager(count, self._stream(), first)
+                self._steps_eager(count, self._stream(), first, advance)
             torch.cuda.current_stream(self.device).wait_stream(s)
             _upload_graph(g, s)
             self._graphs[key] = g
@@ -295,6 +296,21 @@ class TrainEngine:
             out += [(b + k * self.graph_chunk, self.graph_chunk) for k in range(full)]
             if rem:
                 out.append((b + full * self.graph_chunk, rem))
+        return out
+
+    def _cursor_replays(self, first_batch: int, count: int, last_advance: bool = True):
+        """Per window of run(first_batch, count): [(steps, advance), ...] of its cursor-driven
+        graph replays.  last_advance=False: the run's very last graph does not advance the cursor
+        (one node less; for a run no cursor-driven run follows directly -- run() records where
+        the cursor stays, and the next run sets it)."""
+        wins = self.windows(first_batch, count)
+        out = []
+        for wi, (_, n) in enumerate(wins):
+            full, rem = divmod(n, self.graph_chunk)
+            reps = [(self.graph_chunk, True)] * full + ([(rem, True)] if rem else [])
+            if not last_advance and wi == len(wins) - 1 and reps:
+                reps[-1] = (reps[-1][0], False)
+            out.append(reps)
         return out
 
     def capture(self, count: int | None = None):
@@ -322,31 +338,36 @@ class TrainEngine:
             sizes += [self.graph_chunk] * full + ([rem] if rem else [])
         return sizes
 
-    def capture_for(self, first_batch: int, count: int):
-        """Capture (without running) every graph run(first_batch, count) will replay, so no
-        capture lands inside a timed region."""
+    def capture_for(self, first_batch: int, count: int, last_advance: bool = True):
+        """Capture (without running) every graph run(first_batch, count, last_advance=...)
+        will replay, so no capture lands inside a timed region."""
         self._ensure_epoch_mode()
-        if self.graph_absolute and self.graph_chunk > 1:
+        if self.graph_chunk <= 1:
+            return
+        if self.graph_absolute:
             for b, n in self._chunks(first_batch, count):
                 self._graph(n, b)
             return
-        for n in sorted(set(self.graph_sizes(first_batch, count))):
-            self._graph(n)
+        for reps in self._cursor_replays(first_batch, count, last_advance):
+            for n, adv in reps:
+                self._graph(n, advance=adv)
 
     def build_index(self, first_batch: int, count: int):
         """Row index of batches [first_batch, first_batch+count) (one window at most)."""
         _lib.check(self.lib.rae_build_index(self.plan, int(first_batch), int(count), self._stream()),
                    "rae_build_index")
 
-    def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True):
+    def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True,
+            last_advance: bool = True):
         """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
         negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
         of each window of batches is built right before the window's steps (index=False:
         the caller built it already, e.g. bench.py ahead of its timed region).  With graph,
         every step runs inside a replayed HIP graph: graph_chunk-step graphs and one graph
-        per window remainder."""
+        per window remainder (last_advance: see _cursor_replays)."""
         self._ensure_epoch_mode()
-        for b, n in self.windows(first_batch, count):
+        replays = self._cursor_replays(first_batch, count, last_advance)
+        for wi, (b, n) in enumerate(self.windows(first_batch, count)):
             st = self._stream()
             if index:
                 _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
@@ -361,15 +382,12 @@ class TrainEngine:
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
                 self._steps_eager(n, st)
+                self._cursor_at = b + n
             else:
-                full, rem = divmod(n, self.graph_chunk)
-                if full:
-                    g = self._graph(self.graph_chunk)
-                    for _ in range(full):
-                        g.replay()
-                if rem:
-                    self._graph(rem).replay()
-            self._cursor_at = b + n
+                reps = replays[wi]
+                for cnt, adv in reps:
+                    self._graph(cnt, advance=adv).replay()
+                self._cursor_at = b + n - (0 if reps[-1][1] else reps[-1][0])
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):

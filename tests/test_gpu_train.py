@@ -356,7 +356,7 @@ def test_consecutive_runs_skip_cursor_reset(built_lib, cuda_dev):
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     out = []
-    for mode in ("whole", "split", "moved"):
+    for mode in ("whole", "split", "moved", "noadv"):
         data, gold = synthetic_dataset(1200, 900, 5, seed=13)
         ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 40, 24, 12, 5,
                                  0.0, 0.0, "adagrad", "cur", "sp", False, True, False, 1.0,
@@ -369,7 +369,7 @@ def test_consecutive_runs_skip_cursor_reset(built_lib, cuda_dev):
         if mode == "whole":
             eng.run(0, nb)
         else:
-            eng.run(0, 5)
+            eng.run(0, 5, last_advance=(mode != "noadv"))   # noadv: the next run resets it
             if mode == "moved":                     # someone else drove the cursor meanwhile
                 import ctypes as C
                 import torch
