@@ -268,6 +268,7 @@ def main():
     t0 = time.perf_counter()
     # no run follows the timed one on this cursor: its last graph skips the cursor advance
     eng.run(W, K, index=not prebuilt, last_advance=LAST_ADV)
+    t_host = time.perf_counter() - t0          # host time to queue the timed region's work
     torch.cuda.synchronize()
     rdist.barrier()
     torch.cuda.synchronize()
@@ -498,6 +499,7 @@ def main():
         "mfma_bf16_peak": mfma_peak,
         "negative_sampling_s": t_neg,
         "negative_sampling": "host RandomState uniforms (reference stream) + device CDF search",
+        "timed_region_host_queue_us": t_host * 1e6,
         "index_build_us_per_batch": index_us,
         "index_build": ("k_build_index (parameter-independent per-batch row index), built ahead "
                         "of the timed region like the negatives" if prebuilt else
