@@ -157,6 +157,7 @@ class TrainEngine:
         # unknown -- someone else drove it); run() skips its rae_set_cursor launch when the
         # cursor already points at the requested batch (consecutive runs of an epoch)
         self._cursor_at = None
+        self._cursor_reset = os.environ.get("RAE_CURSOR_RESET") == "1"    # A/B: always reset
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -368,20 +369,20 @@ class TrainEngine:
         self._ensure_epoch_mode()
         replays = self._cursor_replays(first_batch, count, last_advance)
         for wi, (b, n) in enumerate(self.windows(first_batch, count)):
-            st = self._stream()
             if index:
-                _lib.check(self.lib.rae_build_index(self.plan, b, n, st), "rae_build_index")
+                _lib.check(self.lib.rae_build_index(self.plan, b, n, self._stream()),
+                           "rae_build_index")
                 if self._index_partitioned:
                     self.check()
             if graph and self.graph_chunk > 1 and self.graph_absolute:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
                 continue
-            if self._cursor_at != b or os.environ.get("RAE_CURSOR_RESET") == "1":
-                _lib.check(self.lib.rae_set_cursor(self.plan, b, st), "rae_set_cursor")
+            if self._cursor_at != b or self._cursor_reset:
+                _lib.check(self.lib.rae_set_cursor(self.plan, b, self._stream()), "rae_set_cursor")
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
-                self._steps_eager(n, st)
+                self._steps_eager(n, self._stream())
                 self._cursor_at = b + n
             else:
                 reps = replays[wi]
