@@ -81,7 +81,27 @@ typedef struct rae_config {
     int64_t index_window;     /* batches whose row index is held at once (0 = default)   */
     int32_t mfma_bf16;        /* RESCAL / hybrid: bf16 MFMA operands for the R/C GEMMs    *
                                * (fp32 accumulate; BASELINE config 5); 0 = exact fp32     */
+    /* kernel forms (0 = the plan's own choice for the shape; the others exist so tests can
+     * pin one form against another -- every form computes the same step):                 */
+    int32_t sp_forward;       /* SP forward: RAE_SPFWD_*                                    */
+    int32_t bil_dp;           /* bilinear dCost/dP contraction: RAE_BILDP_*                 */
+    int32_t bil_prep;         /* bf16 R-gradient operands: RAE_BILPREP_*                    */
+    int32_t dp_update;        /* data-parallel update: RAE_DPUPD_*                          */
 } rae_config;
+
+#define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
+#define RAE_SPFWD_FUSED 1     /* k_forward: one workgroup per example                         */
+#define RAE_SPFWD_SPLIT 2     /* k_sp_enc -> P.C^T GEMM -> k_sp_dec -> dw.C GEMM -> k_sp_fin    */
+#define RAE_BILDP_AUTO 0      /* inside the second M-tile pass when bf16 and m <= 128          */
+#define RAE_BILDP_STRIDED 1   /* k_bil_dp (one wave per 16x16 tile of dP)                      */
+#define RAE_BILDP_STAGED 2    /* k_bil_dp2 (bf16, LDS-staged R slices; r <= 256, m <= 128)      */
+#define RAE_BILDP_MTILE 3     /* inside the second k_bil_mt pass (bf16, m <= 128)               */
+#define RAE_BILPREP_AUTO 0    /* single rank: the forward writes the operands (no launch)      */
+#define RAE_BILPREP_KERNEL 1  /* k_bil_prep after the exchange                                 */
+#define RAE_DPUPD_REPLICATED 0 /* every rank updates every referenced row (bit-identical     *
+                                * replicas after every step)                                  */
+#define RAE_DPUPD_PARTITIONED 1 /* rank k updates the rows it owns (row % G == k) and pushes *
+                                 * the next step's rows to the ranks that read them            */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]
@@ -121,6 +141,11 @@ const char* rae_build_id(void);
 /* floats per example record and per global batch in the exchange buffer */
 int64_t rae_exchange_record_floats(const rae_config* cfg);
 int64_t rae_exchange_floats(const rae_config* cfg);
+
+/* The kernel forms the plan resolved for its shape (RAE_SPFWD_FUSED / _SPLIT, RAE_BILDP_*,
+ * RAE_BILPREP_*, RAE_DPUPD_*; 0 where a form does not apply to the decoder), written into
+ * the matching fields of *out (the other fields are left as they are).                  */
+int rae_plan_forms(const rae_plan* plan, rae_config* out);
 
 /* --- negatives --------------------------------------------------------------------- */
 /* Point the plan at negative-sample arrays (learning/NegativeExampleGenerator.py:14-32

@@ -80,10 +80,10 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
-template <bool BF16>
+template <bool BF16, bool DIRECT = false>
 __global__ __launch_bounds__(RAE_MTT) void k_bil_mt(StepArgs a, int pass) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bil_mt<BF16>(a, pass, smem);
+    bil_mt<BF16, DIRECT>(a, pass, smem);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_DBT) void k_bil_dec(StepArgs a) {
@@ -243,7 +243,6 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
 #define RAE_FIRST(kind_) do { } while (0)
 #endif
     if (wg < nT) {                                            // dense tiles
-#ifndef RAE_SKIP_TILES
         RAE_FIRST(wg < nCt ? 0 : 2);
         if (wg < nCt) {
             const int which = wg / (rt * mt), ti = wg - which * rt * mt;
@@ -255,26 +254,20 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
                          reinterpret_cast<rae_f4*>(spart));
         }
         RAE_WAVE_END();
-#endif
         return;
     }
     if (wg < nT + nP) {                                       // the cost
         const int t = (wg - nT) * RAE_NWAVE + w;
-#ifndef RAE_SKIP_TILES
         if (t == 0) {
             RAE_FIRST(3);
             task_cost(a, lane);
         }
         RAE_WAVE_END();
-#endif
         return;
     }
     // row tasks from the slot's dispatch table (build_batch_tasks): the task entry and the
     // table header are loaded together -- one round trip from wave start to the row's segment
     const int u = wg - nT - nP;
-#ifdef RAE_SKIP_ROWS
-    return;                                                   // diagnostic: dense tasks alone
-#endif
     const int4* thp = reinterpret_cast<const int4*>(a.thdr) + slot;
     if (u < a.NVC) {                                          // very heavy rows
         int4 seg = reinterpret_cast<const int4*>(a.vtask)[slot * a.NVC + u];
@@ -464,6 +457,7 @@ struct rae_plan {
     size_t smem_idx = 0;
     size_t smem_dec = 0;
     size_t smem_mt = 0;     // k_bil_mt: one 8 x 16 x m block of R in LDS
+    bool mt_direct = false; // fp32 blocks beyond LDS (m > 320): k_bil_mt reads R from L2
     bool sp_split = false;  // SP forward as enc -> GEMM -> dec -> GEMM -> fin (large shapes)
     size_t smem_spe = 0;    // k_sp_enc
     bool mt_bf16 = false;
@@ -496,7 +490,14 @@ extern "C" int rae_version(void) { return RAE_VERSION; }
 #ifndef RAE_BUILD_ID
 #define RAE_BUILD_ID "unversioned"
 #endif
-__attribute__((used)) static const char g_build_id[] = "RAE_BUILD_ID:" RAE_BUILD_ID;
+// a diagnostic build (phase stamps, tools/phase_stamps.py) says so in its id: the Python
+// binding loads such a library only when RAE_LIB names it explicitly
+#ifdef RAE_DIAG
+#define RAE_BUILD_KIND "diag-"
+#else
+#define RAE_BUILD_KIND ""
+#endif
+__attribute__((used)) static const char g_build_id[] = "RAE_BUILD_ID:" RAE_BUILD_KIND RAE_BUILD_ID;
 extern "C" const char* rae_build_id(void) { return g_build_id + 13; }
 
 extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
@@ -519,6 +520,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "relations must be in [1, 1024]");
     if (c.embed < 1 || c.embed > 1024) return fail(RAE_E_INVALID, "embed must be in [1, 1024]");
     if (c.neg_samples < 1) return fail(RAE_E_INVALID, "neg_samples must be >= 1");
+    if (c.sp_forward < RAE_SPFWD_AUTO || c.sp_forward > RAE_SPFWD_SPLIT ||
+        c.bil_dp < RAE_BILDP_AUTO || c.bil_dp > RAE_BILDP_MTILE ||
+        c.bil_prep < RAE_BILPREP_AUTO || c.bil_prep > RAE_BILPREP_KERNEL ||
+        c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED)
+        return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update)");
+    if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
+        return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.batch_size < 1 || c.world_size < 1 || c.rank < 0 || c.rank >= c.world_size)
         return fail(RAE_E_INVALID, "bad batch_size/world_size/rank");
     if (c.n_examples < (int64_t)c.batch_size * c.world_size)
@@ -660,34 +668,33 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
     // bf16 dP with LDS-staged R slices (k_bil_dp2): the C5 shape compiled exactly, other
     // shapes up to r = 256, K = 128 padded; float4 rows needed (r, K multiples of 4)
+    // dP contraction form: in the second M-tile pass (bf16, m <= 128) by default; k_bil_dp2
+    // (bf16, LDS-staged R slices: the C5 shape compiled exactly, others up to r = 256, m = 128
+    // padded; float4 rows) or the strided k_bil_dp otherwise / on request
+    const bool mt_ok = bil && c.mfma_bf16 && c.relations <= 128;
+    const bool dp2_ok = a.bf16 && c.embed % 4 == 0 && c.relations % 4 == 0 &&
+                        (((c.embed + 31) / 32 == 7 && (c.relations + 15) / 16 == 7) ||
+                         (c.embed <= 256 && c.relations <= 128));
+    const bool mtdp = mt_ok && (c.bil_dp == RAE_BILDP_AUTO || c.bil_dp == RAE_BILDP_MTILE);
     p->dp2 = 0;
-    const char* dp2env = getenv("RAE_DP2");      // diagnostic override: 0 = strided kernel
-    if (a.bf16 && c.embed % 4 == 0 && c.relations % 4 == 0 && !(dp2env && dp2env[0] == '0')) {
-        if ((c.embed + 31) / 32 == 7 && (c.relations + 15) / 16 == 7) p->dp2 = 1;
-        else if (c.embed <= 256 && c.relations <= 128) p->dp2 = 2;
-    }
+    if (!mtdp && dp2_ok && c.bil_dp != RAE_BILDP_STRIDED)
+        p->dp2 = ((c.embed + 31) / 32 == 7 && (c.relations + 15) / 16 == 7) ? 1 : 2;
     a.nib = bil ? (p->dp2 ? (c.embed + RAE_IB2 - 1) / RAE_IB2 : (c.embed + RAE_IB - 1) / RAE_IB) : 0;
     const size_t o_dpp = bil ? take(4ull * a.nib * c.batch_size * c.relations) : 0;
     a.r4 = align4(c.embed);
     const int64_t nbi_mt = (c.embed + RAE_MTI - 1) / RAE_MTI, nbj_mt = (c.embed + RAE_MTJ - 1) / RAE_MTJ;
     const size_t o_mtv = bil ? take(4ull * nbj_mt * c.batch_size * a.r4) : 0;
     const size_t o_mtw = bil ? take(4ull * nbi_mt * c.batch_size * a.r4) : 0;
-    // dP inside the second k_bil_mt pass (bf16 blocks; RAE_MTDP=0 keeps k_bil_dp2 / k_bil_dp)
-    const char* mtdpenv = getenv("RAE_MTDP");
-    const bool mtdp = bil && c.mfma_bf16 && c.relations <= 128 && !(mtdpenv && mtdpenv[0] == '0');
     a.nmtp = (int)(nbi_mt * nbj_mt);
     const size_t o_mtp = mtdp ? take(4ull * a.nmtp * c.batch_size * c.relations) : 0;
     // split SP forward (rae_sp_split.hpp) for runtime shapes whose decoder matrices stream
-    // through every example's workgroup (r*m > RAE_SPLIT_RM; C4: 90 k); RAE_SPSPLIT=0/1 forces
-    const char* splitenv = getenv("RAE_SPSPLIT");
-    p->sp_split = !bil && (int64_t)c.embed * c.relations > RAE_SPLIT_RM;
-    if (splitenv && (splitenv[0] == '0' || splitenv[0] == '1')) p->sp_split = !bil && splitenv[0] == '1';
+    // through every example's workgroup (r*m > RAE_SPLIT_RM; C4: 90 k), or on request
+    p->sp_split = !bil && (c.sp_forward == RAE_SPFWD_SPLIT ||
+                           (c.sp_forward == RAE_SPFWD_AUTO &&
+                            (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
     const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
     a.Lp = (L + 31) / 32 * 32;
-    {
-        const char* fp = getenv("RAE_FUSEPREP");     // A/B override: 0 keeps k_bil_prep
-        a.fuse_prep = (a.bf16 && c.world_size == 1 && !(fp && fp[0] == '0')) ? 1 : 0;
-    }
+    a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
@@ -735,11 +742,15 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
     p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
     p->smem_mt = bil ? bil_mt_lds_bytes(c.relations, p->mt_bf16) : 0;
-    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024 ||
-        p->smem_mt > 160 * 1024) {
+    if (p->smem_mt > RAE_MT_LDS_MAX) {        // fp32 block too large to stage (m > 320)
+        p->mt_direct = true;
+        p->smem_mt = 0;
+    }
+    if (p->smem_fwd > 160 * 1024 || p->smem_idx > 160 * 1024 || p->smem_dec > 160 * 1024) {
         (void)hipFree(p->ws);
         delete p;
-        return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example");
+        return fail(RAE_E_INVALID, "configuration needs more than 160 KiB LDS per example "
+                                   "workgroup (relations / embed / neg_samples too large)");
     }
     p->grid_fwd = c.batch_size;
     const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC);
@@ -783,6 +794,18 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
     }
     *out = p;
+    return RAE_OK;
+}
+
+extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
+    if (!p || !out) return fail(RAE_E_INVALID, "null argument");
+    const bool bil = p->cfg.decoder != RAE_DEC_SP;
+    out->sp_forward = bil ? 0 : (p->sp_split ? RAE_SPFWD_SPLIT : RAE_SPFWD_FUSED);
+    out->bil_dp = !bil ? 0 : (p->args.mtP ? RAE_BILDP_MTILE
+                              : (p->dp2 ? RAE_BILDP_STAGED : RAE_BILDP_STRIDED));
+    out->bil_prep = (!bil || !p->args.bf16) ? 0 : (p->args.fuse_prep ? RAE_BILPREP_AUTO
+                                                                    : RAE_BILPREP_KERNEL);
+    out->dp_update = p->cfg.dp_update;
     return RAE_OK;
 }
 
@@ -849,11 +872,12 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
     RAE_LAUNCH(p, (k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
     const dim3 gmt(((a.r + RAE_MTI - 1) / RAE_MTI) * ((a.r + RAE_MTJ - 1) / RAE_MTJ));
-    if (p->mt_bf16) RAE_LAUNCH(p, k_bil_mt<true>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 0);
-    else RAE_LAUNCH(p, k_bil_mt<false>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 0);
-    RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
-    if (p->mt_bf16) RAE_LAUNCH(p, k_bil_mt<true>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
-    else RAE_LAUNCH(p, k_bil_mt<false>, gmt, dim3(RAE_MTT), p->smem_mt, st, a, 1);
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
+        if (p->mt_bf16) RAE_LAUNCH(p, (k_bil_mt<true>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
+        else if (p->mt_direct) RAE_LAUNCH(p, (k_bil_mt<false, true>), gmt, dim3(RAE_MTT), 0, st, a, pass);
+        else RAE_LAUNCH(p, (k_bil_mt<false>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
+    }
     if (!a.mtP) launch_fwd_dp(p, a, st);              // else dP came with the second pass
     RAE_LAUNCH(p, k_bil_fin, ge, dim3(RAE_FINT), 0, st, a);
 }

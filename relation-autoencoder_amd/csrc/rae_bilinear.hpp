@@ -149,6 +149,9 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
     return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 + (size_t)KP * RAE_MT_TP * 2
                 : (size_t)RAE_MTI * RAE_MTJ * m * 4;
 }
+// fp32 blocks are 512 m bytes: above m = 320 they exceed the 160 KiB of LDS, and the block's
+// MFMA chains read R straight from global memory (L2) instead (bil_mt<false, true>)
+#define RAE_MT_LDS_MAX (160 * 1024)
 #ifndef RAE_MT_STAMP_PASS
 #define RAE_MT_STAMP_PASS 0
 #endif
@@ -162,8 +165,9 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
 #define RAE_MT_STAMP(slot) do { } while (0)
 #endif
 
-template <bool BF16>
+template <bool BF16, bool DIRECT = false>
 __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
+    static_assert(!(BF16 && DIRECT), "bf16 blocks are always staged (m <= 128)");
     const int r = a.r, m = a.m, l = a.l;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -176,7 +180,9 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     __bf16* sT = reinterpret_cast<__bf16*>(smem) + RAE_MTI * RAE_MTJ * ST;
     RAE_MT_STAMP(0);
     // ---- stage: LDS row (ii, jj) = R[i0+ii][j0+jj][0..m); rows past r are zero
-    if ((m & 3) == 0) {
+    if (DIRECT) {
+        // no staging: the MFMA chains read the block's rows from global memory
+    } else if ((m & 3) == 0) {
         const int m4 = m / 4, nv = RAE_MTI * RAE_MTJ * m4;
         for (int e0 = 0; e0 < nv; e0 += RAE_MTT * RAE_MT_SB) {
             float4 v[RAE_MT_SB];
@@ -290,6 +296,16 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sf, pf[ks], acc, 0, 0, 0);
                     }
                 }
+            } else if (DIRECT) {
+                const int i = i0 + ii, j = j0 + li;
+                const bool rv = i < r && j < r;
+                const float* grow = a.R3 + ((int64_t)(rv ? i : 0) * r + (rv ? j : 0)) * m;
+                for (int k0 = 0; k0 < m; k0 += 4) {
+                    const int k = k0 + g;
+                    const float sa = (rv && k < m) ? grow[k] : 0.f;
+                    const float pb = (bv && k < m) ? Pa[k] : 0.f;
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sa, pb, acc, 0, 0, 0);
+                }
             } else {
                 const float* srow = reinterpret_cast<const float*>(smem) + (ii * RAE_MTJ + li) * ST;
                 for (int k0 = 0; k0 < m; k0 += 4) {
@@ -390,9 +406,6 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg) {     // D[b = 4g + reg][k = li]
                         const int bo = bt * 16 + 4 * g + reg;
-#ifdef RAE_MT_NODPST      // diagnostic: dP computed, not stored
-                        if (a.lr == -12345.f)
-#endif
                         if (bo < l && k < m)
                             a.mtP[((int64_t)blockIdx.x * l + bo) * m + k] = dacc[kt][reg];
                     }

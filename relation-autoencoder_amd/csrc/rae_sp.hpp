@@ -180,21 +180,12 @@ struct CCache {
         const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
 #pragma unroll
         for (int ra = 0; ra < RA; ++ra) {
-#ifdef RAE_C_HOT
-            const int i = (gid + RAE_NG * ra) & 7;   // diagnostic: 8 hot rows (L1 hits)
-#else
             const int i = min(r0 + gid + RAE_NG * ra, Dm.r - 1);
-#endif
 #pragma unroll
             for (int cc = 0; cc < CC; ++cc) {
                 const int c = min(c0 + q + 16 * cc, mv - 1);
-#ifdef RAE_SKIP_C
-                vzero(c1[ra][cc]);     // diagnostic: no decoder-matrix traffic
-                vzero(c2[ra][cc]);
-#else
                 c1[ra][cc] = C1v[i * mv + c];
                 c2[ra][cc] = C2v[i * mv + c];
-#endif
             }
         }
     }
@@ -621,17 +612,8 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 4);
 
     // scores, loss, coefficients (wave 0)
-#ifdef RAE_ICACHE_TEST
-#pragma clang loop unroll(disable)
-    for (int rep = 0; rep < 2; ++rep) {
-    if (rep == 1) RAE_STAMP(a, 10);
-#endif
     sp_coefficients(a, Dm, S, H);
     __syncthreads();
-#ifdef RAE_ICACHE_TEST
-    if (rep == 1) RAE_STAMP(a, 11);
-    }
-#endif
     RAE_STAMP(a, 8);
 
     // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
@@ -728,11 +710,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         for (int k = 0; k < KF; ++k) {
             const int f = slot + NSL * k;
             const bool ok = slot < NSL && f < nf;
-#ifdef RAE_W_ROW0
-            const int fi = 0;                  // diagnostic: every W row from row 0 (cache hits)
-#else
             const int fi = S.sfidx[f < 256 ? f : 255];
-#endif
             wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
             fv[k] = ok ? S.sfval[f < 256 ? f : 255] : 0.f;
         }

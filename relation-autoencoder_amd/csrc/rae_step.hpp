@@ -131,6 +131,9 @@ __device__ __forceinline__ int64_t step_batch(const StepArgs& a) {
     return a.cursor ? *a.cursor + a.step_offset : a.step_offset;
 }
 
+#if defined(RAE_STAMPS) && !defined(RAE_DIAG)
+#error "RAE_STAMPS instruments the kernels for tools/phase_stamps.py: a diagnostic build (-DRAE_DIAG)"
+#endif
 #ifdef RAE_STAMPS
 #define RAE_STAMP(a, slot)                                                                  \
     do {                                                                                    \

@@ -73,7 +73,7 @@ EXPORTS = (
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
-    "rae_stream_copy", "rae_mfma_probe",
+    "rae_stream_copy", "rae_mfma_probe", "rae_plan_forms",
 )
 
 
@@ -87,7 +87,18 @@ class RaeConfig(C.Structure):
         ("lambda2", C.c_float), ("ext_reg", C.c_int32), ("max_batch_nnz", C.c_int32),
         ("max_row_nnz", C.c_int32), ("neg_mode", C.c_int32), ("neg_stride", C.c_int64),
         ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
+        ("sp_forward", C.c_int32), ("bil_dp", C.c_int32), ("bil_prep", C.c_int32),
+        ("dp_update", C.c_int32),
     ]
+
+
+# kernel forms (include/rae.h RAE_SPFWD_* / RAE_BILDP_* / RAE_BILPREP_* / RAE_DPUPD_*)
+KERNEL_FORMS = {
+    "sp_forward": {"auto": 0, "fused": 1, "split": 2},
+    "bil_dp": {"auto": 0, "strided": 1, "staged": 2, "mtile": 3},
+    "bil_prep": {"auto": 0, "kernel": 1},
+    "dp_update": {"replicated": 0, "partitioned": 1},
+}
 
 
 _P = C.c_void_p
@@ -135,6 +146,7 @@ def load(path: str | None = None):
     lib.rae_exchange_floats.argtypes = [C.POINTER(RaeConfig)]
     lib.rae_plan_create.argtypes = [C.POINTER(RaeConfig), C.POINTER(RaeBuffers), C.POINTER(_P)]
     lib.rae_plan_destroy.argtypes = [_P]
+    lib.rae_plan_forms.argtypes = [_P, C.POINTER(RaeConfig)]
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]
     lib.rae_advance_cursor.argtypes = [_P, C.c_int64, _P]
@@ -157,7 +169,7 @@ def load(path: str | None = None):
     lib.rae_event_destroy.argtypes = [_P]
     lib.rae_event_elapsed_ms.argtypes = [_P, _P, C.POINTER(C.c_float)]
     for fn in ("rae_stream_copy", "rae_mfma_probe", "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
-               "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_set_negatives", "rae_set_cursor",
+               "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_plan_forms", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
                "rae_step_forward_at", "rae_step_update_at",
                "rae_check", "rae_label", "rae_build_index"):

@@ -68,7 +68,8 @@ class DeviceSplit:
 class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
-                 index_window=0, device=None, mfma_bf16=False):
+                 index_window=0, device=None, mfma_bf16=False, kernel_forms=None,
+                 graph_absolute=False):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -111,6 +112,13 @@ class TrainEngine:
         cfg.neg_stride = self.N
         cfg.index_window = int(index_window)
         cfg.mfma_bf16 = 1 if mfma_bf16 else 0
+        # kernel forms (include/rae.h RAE_SPFWD_* ...): {"sp_forward": "split", ...}; the
+        # plan picks for the shape when a form is not named
+        self.kernel_forms = dict(kernel_forms or {})
+        for key, val in self.kernel_forms.items():
+            if key not in _lib.KERNEL_FORMS or val not in _lib.KERNEL_FORMS[key]:
+                raise ValueError(f"unknown kernel form {key}={val!r}")
+            setattr(cfg, key, _lib.KERNEL_FORMS[key][val])
         self.cfg = cfg
         self.rec_floats = int(self.lib.rae_exchange_record_floats(C.byref(cfg)))
         self.exchange_buf = torch.zeros(int(self.lib.rae_exchange_floats(C.byref(cfg))),
@@ -152,12 +160,13 @@ class TrainEngine:
         # (rae_step_*_at: no dependent device-cursor load at kernel start), one graph per
         # graph_chunk-step chunk of the epoch; otherwise one graph per chunk size, replayed
         # along the epoch by the device cursor
-        self.graph_absolute = os.environ.get("RAE_GRAPH_ABS", "0") == "1"
+        self.graph_absolute = bool(graph_absolute)
         # batch the device cursor holds after this engine's last cursor-driven run (None:
-        # unknown -- someone else drove it); run() skips its rae_set_cursor launch when the
-        # cursor already points at the requested batch (consecutive runs of an epoch)
+        # unknown); run() skips its rae_set_cursor launch when the cursor already points at
+        # the requested batch (consecutive runs of an epoch).  Every cursor move goes through
+        # this engine (set_cursor / run); a caller driving the plan directly calls
+        # cursor_moved() afterwards.
         self._cursor_at = None
-        self._cursor_reset = os.environ.get("RAE_CURSOR_RESET") == "1"    # A/B: always reset
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -174,6 +183,26 @@ class TrainEngine:
             self.close()
         except Exception:
             pass
+
+    def kernel_forms_in_use(self):
+        """The kernel forms the plan resolved for its shape (rae_plan_forms): sp_forward
+        fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep fused|kernel
+        (bf16 bilinear), dp_update; None where a form does not apply."""
+        out = _lib.RaeConfig()
+        _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
+        F = _lib.KERNEL_FORMS
+        name = {key: {code: n for n, code in F[key].items()} for key in F}
+        sp = self.cfg.decoder == 0
+        bf16 = not sp and bool(self.cfg.mfma_bf16)
+        return {"sp_forward": name["sp_forward"][out.sp_forward] if sp else None,
+                "bil_dp": name["bil_dp"][out.bil_dp] if not sp else None,
+                "bil_prep": ("kernel" if out.bil_prep == 1 else "fused") if bf16 else None,
+                "dp_update": name["dp_update"][out.dp_update]}
+
+    def set_cursor(self, batch: int):
+        """Point the device cursor at global batch `batch` (stream-ordered)."""
+        _lib.check(self.lib.rae_set_cursor(self.plan, int(batch), self._stream()), "rae_set_cursor")
+        self._cursor_at = int(batch)
 
     def cursor_moved(self):
         """Tell the engine the device cursor was driven outside run() (direct rae_set_cursor /
@@ -378,8 +407,8 @@ class TrainEngine:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
                 continue
-            if self._cursor_at != b or self._cursor_reset:
-                _lib.check(self.lib.rae_set_cursor(self.plan, b, self._stream()), "rae_set_cursor")
+            if self._cursor_at != b:
+                self.set_cursor(b)
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
                 self._steps_eager(n, self._stream())

@@ -53,7 +53,8 @@ class ReconstructInducer:
                  embed_size, nb_relations, nb_neg_samples, lambda1, lambda2, optimization,
                  model_name, decoder_model, external_embeddings, extended_regularizer,
                  frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
-                 graph_chunk=64, neg_sampler="device", neg_seed=0, mfma_bf16=False):
+                 graph_chunk=64, neg_sampler="device", neg_seed=0, mfma_bf16=False,
+                 kernel_forms=None):
         self.data = data
         self.goldStandard = gold_standard
         self.rng = rng
@@ -82,6 +83,7 @@ class ReconstructInducer:
         self.neg_sampler = neg_sampler     # host / device: the reference's RNG stream
         self.neg_seed = int(neg_seed)
         self.mfma_bf16 = bool(mfma_bf16)   # RESCAL / hybrid: bf16 MFMA operands (config 5)
+        self.kernel_forms = dict(kernel_forms or {})   # engine.TrainEngine kernel_forms
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
                         f"_embedsize{embed_size}_l1{lambda1}_l2{lambda2}_opt{optimization}"
@@ -144,7 +146,7 @@ class ReconstructInducer:
                                   lambda2=self.lambdaL2, world_size=self.world_size,
                                   rank=self.rank, exchange=self.exchange,
                                   graph_chunk=self.graph_chunk, device=self.device,
-                                  mfma_bf16=self.mfma_bf16)
+                                  mfma_bf16=self.mfma_bf16, kernel_forms=self.kernel_forms)
         self.func["train"] = _TrainFunction(self.engine)
         for key in self.data.generate_split_keys():
             ds = self.engine.split if key == "train" else DeviceSplit(self.data.split[key], self.device)

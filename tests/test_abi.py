@@ -51,3 +51,52 @@ def test_plan_create_rejects_bad_config(built_lib):
     rc = built_lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(h))
     assert rc == -1
     assert b"decoder" in built_lib.rae_last_error()
+
+
+def test_struct_offsets_match_c_compiler(tmp_path):
+    """Every rae_config / rae_buffers field sits at the offset the C compiler gives it."""
+    import subprocess
+    from rae import _lib
+    src = tmp_path / "off.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rae.h"', "int main(void) {"]
+    for cname, cls in (("rae_config", _lib.RaeConfig), ("rae_buffers", _lib.RaeBuffers)):
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(line.rsplit(" ", 1) for line in
+               subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+               if line)
+    for cname, cls in (("rae_config", _lib.RaeConfig), ("rae_buffers", _lib.RaeBuffers)):
+        assert int(got[cname]) == C.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
+
+
+def test_shipped_library_is_not_a_diagnostic_build(built_lib):
+    """The in-tree library is the product build: its id is the hash of the sources beside it
+    (no -DRAE_DIAG phase-stamp instrumentation, which says 'diag-' in the id), and the kernel
+    sources read no environment variables (every kernel form is a rae_config field)."""
+    from rae import _lib
+    bid = _lib.library_build_id()
+    assert bid == _lib.source_build_id()
+    assert not bid.startswith("diag")
+    for f in _lib.source_files():
+        txt = open(f).read()
+        assert "getenv" not in txt, f
+
+
+def test_plan_create_rejects_unknown_kernel_form(built_lib):
+    from rae import _lib
+    cfg = _lib.RaeConfig()
+    cfg.decoder, cfg.relations, cfg.embed, cfg.neg_samples = 0, 8, 8, 2
+    cfg.batch_size, cfg.world_size, cfg.n_examples = 4, 1, 8
+    cfg.sp_forward = 9
+    bufs = _lib.RaeBuffers()
+    h = C.c_void_p()
+    assert built_lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(h)) == -1
+    assert b"kernel form" in built_lib.rae_last_error()

@@ -140,22 +140,19 @@ def test_synthetic_vs_oracle(built_lib, cuda_dev, shape):
     dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10, force=True),
     dict(N=200, d=3000, m=300, r=300, s=50, l=100, ntrue=10, epochs=1),  # C4 K/r/s: split by default
 ], ids=["small", "odd", "c3shape", "c4shape"])
-def test_split_sp_forward_vs_oracle(built_lib, cuda_dev, shape, monkeypatch):
+def test_split_sp_forward_vs_oracle(built_lib, cuda_dev, shape):
     """The split SP forward (rae_sp_split.hpp: encoder, P.C^T GEMM, decoder, dw.C GEMM,
     softmax backward as five kernels) against the float64 oracle, with the same tolerances as
     the fused example kernel."""
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
-    if shape.get("force"):
-        monkeypatch.setenv("RAE_SPSPLIT", "1")
-    else:
-        monkeypatch.delenv("RAE_SPSPLIT", raising=False)
+    forms = {"sp_forward": "split"} if shape.get("force") else {}
     data, gold = synthetic_dataset(shape["N"], shape["d"], shape["ntrue"], seed=99)
     m, r, s, l = shape["m"], shape["r"], shape["s"], shape["l"]
     ep = shape.get("epochs", 2)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), ep, 0.1, l, r, m, s, 0.0, 0.0,
                              "adagrad", "split", "sp", False, True, False, 1.0, device=cuda_dev,
-                             graph_chunk=2)
+                             graph_chunk=2, kernel_forms=forms)
     ind.learn(verbose=False)
     tr, costs = _oracle_trajectory("sp", data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
     np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
@@ -389,9 +386,9 @@ def test_consecutive_runs_skip_cursor_reset(built_lib, cuda_dev):
 
 @pytest.mark.parametrize("shape", [(100, 200, 20, 100), (60, 96, 5, 40)], ids=["c5", "padded"])
 @pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
-def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
+def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape):
     """The LDS-staged bf16 dP kernel (k_bil_dp2, compiled for the C5 shape and padded for
-    others) against the strided bf16 kernel it replaces (RAE_DP2=0): the same bf16 operands,
+    others) against the strided bf16 kernel it replaces (bil_dp="strided"): the same bf16 operands,
     only the fp32 summation order differs, so whole runs agree to 5e-4 relative Frobenius
     distance -- far inside the bf16-vs-float64 tolerance above (which both kernels meet
     equally: tools/bf16_check.py).  Two batches only: over longer runs the drift between the
@@ -401,14 +398,13 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
     from rae.inducer import ReconstructInducer
     m, r, s, l = shape
     out = []
-    monkeypatch.setenv("RAE_MTDP", "0")       # dP from k_bil_dp2 / k_bil_dp, not k_bil_mt
-    for flag in ("1", "0"):
-        monkeypatch.setenv("RAE_DP2", flag)
+    for form in ("staged", "strided"):        # dP from k_bil_dp2 / k_bil_dp, not k_bil_mt
         # two batches: longer runs amplify the summation-order difference chaotically
         data, gold = synthetic_dataset(2 * l, 2000, 10, seed=99)
         ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0,
                                  0.0, "adagrad", "dp2", dec, False, True, False, 1.0,
-                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True)
+                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True,
+                                 kernel_forms={"bil_dp": form})
         ind.learn(verbose=False)
         out.append((_params(ind), np.array(ind.epoch_costs)))
     # the per-batch costs drift with the parameters (up to 2.6e-5 relative seen)
@@ -422,20 +418,20 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape, monkeypatch):
 @pytest.mark.parametrize("shape", [(100, 200, 20, 100), (60, 96, 5, 40), (20, 50, 3, 30)],
                          ids=["c5", "padded", "ragged"])
 @pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
-def test_bf16_dp_in_mtile_pass_agrees(built_lib, cuda_dev, dec, shape, monkeypatch):
+def test_bf16_dp_in_mtile_pass_agrees(built_lib, cuda_dev, dec, shape):
     """dP computed inside the second k_bil_mt pass (per 8x16 block of R, partials summed by
-    k_bil_fin) against k_bil_dp2 / k_bil_dp (RAE_MTDP=0): the same bf16 operands, another fp32
+    k_bil_fin) against k_bil_dp2 / k_bil_dp (bil_dp="staged"): the same bf16 operands, another fp32
     summation order -> two batches agree to 5e-4 relative (as test_bf16_dp_kernels_agree)."""
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     m, r, s, l = shape
     out = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("RAE_MTDP", flag)
+    for form in ("mtile", "staged"):
         data, gold = synthetic_dataset(2 * l, 2000, 10, seed=99)
         ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0,
                                  0.0, "adagrad", "mtdp", dec, False, True, False, 1.0,
-                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True)
+                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True,
+                                 kernel_forms={"bil_dp": form})
         ind.learn(verbose=False)
         out.append((_params(ind), np.array(ind.epoch_costs)))
     np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-4, atol=2e-6)

@@ -33,7 +33,7 @@ def build_diag():
     src = os.path.join(PKG, "csrc", "rae.hip")
     _lib = ge._lib_mod()
     if not os.path.exists(DIAG) or os.path.getmtime(DIAG) < max(os.path.getmtime(s) for s in _lib.source_files()):
-        subprocess.run([ge.HIPCC, *_lib.BUILD_FLAGS, "-DRAE_STAMPS", *VARIANT.split(), src, "-o", DIAG],
+        subprocess.run([ge.HIPCC, *_lib.BUILD_FLAGS, "-DRAE_STAMPS", "-DRAE_DIAG", *VARIANT.split(), src, "-o", DIAG],
                        check=True)
 
 

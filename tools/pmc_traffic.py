@@ -80,6 +80,12 @@ def main():
         if g:
             groups[g] += v["traffic_bytes"]
     out.update(groups)
+    # the library the passes profiled (bench.py compares it with the one it runs)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "relation-autoencoder_amd"))
+    from rae import _lib
+    out["build_id"] = _lib.library_build_id()
     txt = json.dumps(out, indent=1)
     print(txt)
     if args.out:
