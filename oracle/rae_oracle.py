@@ -171,8 +171,24 @@ class StepResult:
     grads: dict = field(default_factory=dict)   # dense, param-shaped
 
 
-def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D):
-    """Returns (scores_without_entropy_parts, dP, grads-dict) for the decoder."""
+def bf16_round(x):
+    """Round to bfloat16 (nearest even, via float32) and back to float64: the operand
+    rounding of v_mfma_f32_16x16x32_bf16 (no NaN/inf inputs here)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D, bf16=False):
+    """Returns (scores_without_entropy_parts, dP, grads-dict) for the decoder.
+
+    bf16 (bilinear decoders only): emulate rae_config.mfma_bf16 -- the three R contractions
+    take bf16-rounded operands (fp32 / here float64 accumulation), exactly where the MI355X
+    kernels round: M = P.R (k_bil_mt: bf16 P and R), dP = sum_ij U_ij R_ij (U = x a2^T + a1 y^T
+    formed in fp32, then rounded), dR = sum_b P_b U_b (U formed from bf16 copies of x, a1, a2,
+    y, then rounded; P bf16).  Not the reference's arithmetic: it measures how far bf16
+    operands alone move a trajectory, which is what the bf16 path's tolerance is derived from
+    (tests/test_gpu_fullscale.py)."""
     A, Ab = p["A"], p["Ab"]
     l = P.shape[0]
     s = neg1.shape[0]
@@ -219,8 +235,11 @@ def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D):
         dP = dwC1 @ C1 + dwC2 @ C2
     else:
         Rk = p["R"] if decoder == "rescal" else p["C"]      # (r, r, m)
+        r_ = Rk.shape[0]
         a2 = A[e2]
-        M = np.einsum("bk,ijk->bij", P, Rk)        # Bilinear.py:33 / BilinearPlusSP.py:37
+        # M_b = sum_k P_bk R[:,:,k]  (Bilinear.py:33 / BilinearPlusSP.py:37) as one GEMM
+        Rb = (bf16_round(Rk) if bf16 else Rk).reshape(r_ * r_, -1)
+        M = ((bf16_round(P) if bf16 else P) @ Rb.T).reshape(l, r_, r_)
         Ma2 = np.einsum("bij,bj->bi", M, a2)        # M a2
         MTa1 = np.einsum("bij,bi->bj", M, a1)       # M^T a1
         one = np.einsum("bi,bi->b", a1, Ma2)        # Bilinear.py:58-59
@@ -252,8 +271,16 @@ def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D):
         g_a2 = np.einsum("bij,bi->bj", M, x)
         g_n1 = dg1.T[..., None] * Ma2[None]          # (s, l, r)
         g_n2 = dg2.T[..., None] * MTa1[None]
-        gR = np.einsum("bk,bi,bj->ijk", P, x, a2) + np.einsum("bk,bi,bj->ijk", P, a1, y)
-        dP = np.einsum("bi,ijk,bj->bk", x, Rk, a2) + np.einsum("bi,ijk,bj->bk", a1, Rk, y)
+        # U_b = dCost/dM_b = x_b a2_b^T + a1_b y_b^T;  dP_bk = <U_b, R_k>;  dR_k = sum_b P_bk U_b
+        U = (x[:, :, None] * a2[:, None, :] + a1[:, :, None] * y[:, None, :]).reshape(l, -1)
+        if bf16:
+            dP = bf16_round(U) @ Rb
+            bx, b1, b2, by = bf16_round(x), bf16_round(a1), bf16_round(a2), bf16_round(y)
+            Uf = (bx[:, :, None] * b2[:, None, :] + b1[:, :, None] * by[:, None, :]).reshape(l, -1)
+            gR = (bf16_round(Uf).T @ bf16_round(P)).reshape(r_, r_, -1)
+        else:
+            dP = U @ Rb
+            gR = (U.T @ P).reshape(r_, r_, -1)
         if decoder == "rescal+sp":
             c_a1 = dOne + dg2.sum(1)     # <wC1,a1> appears in one and in every negRight
             c_a2 = dOne + dg1.sum(1)     # <wC2,a2> appears in one and in every negLeft
@@ -285,7 +312,8 @@ def _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D):
 
 def train_step_grads(decoder: str, p: dict, X, e1, e2, neg1, neg2, *, alpha: float,
                      lambda1: float = 0.0, lambda2: float = 0.0, adjust: float = 0.0,
-                     ext_reg: bool = True, denom: float | None = None) -> StepResult:
+                     ext_reg: bool = True, denom: float | None = None,
+                     bf16: bool = False) -> StepResult:
     """Forward + loss + dense gradients of one ``func['train']`` call.
 
     cost = -mean(all_scores) + lambda1*adjust*L1 + lambda2*adjust*L2
@@ -304,7 +332,8 @@ def train_step_grads(decoder: str, p: dict, X, e1, e2, neg1, neg2, *, alpha: flo
         D = denom
     S, P, logP = encoder_forward(X, p["W"], p["Wb"])
     H = alpha * -(P * logP).sum(axis=1)                     # OieModel.py:81
-    pos, negs, dP, g = _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D)
+    pos, negs, dP, g = _decoder_forward_backward(decoder, p, P, H, e1, e2, neg1, neg2, D,
+                                                 bf16=bf16)
     scores = np.concatenate([pos, H, H, negs])
     assert scores.shape[0] == 4 * l + 2 * l * s
     cost = -float(scores.sum()) / D                         # OieModel.py:90 (mean)
@@ -365,6 +394,7 @@ class OracleTrainer:
     optimizer: str = "adagrad"
     ext_reg: bool = True
     dtype: type = np.float64
+    bf16: bool = False          # emulate the bf16-operand R contractions (see bf16_round)
 
     def __post_init__(self):
         n = len(self.cum)
@@ -380,7 +410,7 @@ class OracleTrainer:
         res = train_step_grads(self.decoder, self.params, self.X[rows], self.args1[rows],
                                self.args2[rows], neg1, neg2, alpha=self.alpha,
                                lambda1=self.lambda1, lambda2=self.lambda2,
-                               adjust=self.adjust, ext_reg=self.ext_reg)
+                               adjust=self.adjust, ext_reg=self.ext_reg, bf16=self.bf16)
         if self.optimizer == "adagrad":
             adagrad_apply(self.params, self.acc, res.grads, self.lr)
         elif self.optimizer == "sgd":

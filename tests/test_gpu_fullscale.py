@@ -51,6 +51,102 @@ def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234):
     return np.array(want), got, tr.params, params, init
 
 
+def test_c2_full_size(built_lib, cuda_dev):
+    # BASELINE config 2 at its real size: 100k synthetic triples, d = 2^17, K = 30, embed 100,
+    # neg 10, l = 100 (the compile-time C2 specialisation of the forward, scalar lanes: K is
+    # not a multiple of 4)
+    want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=100_000, d=2 ** 17, m=30, r=100,
+                                              s=10, l=100, ntrue=30, steps=6)
+    _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
+
+
+# --------------------------------------------------------------------------------------------
+# bf16 MFMA operands (BASELINE config 5): the tolerance is derived per trajectory
+# --------------------------------------------------------------------------------------------
+def bf16_trajectories(cuda_dev, dec, N, d, m, r, s, l, ntrue, steps, seed_data=1234,
+                      graph_chunk=2):
+    """The GPU bf16 path, the exact float64 oracle and the float64 oracle with the bf16
+    operand rounding emulated (rae_oracle.bf16_round at the three R contractions), over the
+    same first `steps` batches of an epoch from RandomState(2).  Returns dict of
+    costs / params per run ("gpu", "exact", "emu") and the initial parameters."""
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    data, gold = synthetic_dataset(N, d, ntrue, seed=seed_data)
+    xs = data.split["train"]
+    out = {}
+    for name, bf in (("exact", False), ("emu", True)):
+        tr = O.OracleTrainer(dec, xs.xFeats, xs.args1, xs.args2, data.negSamplingCum,
+                             np.random.RandomState(2), m, r, s, l, lr=0.1, alpha=1.0, bf16=bf)
+        if name == "exact":
+            init = {k: v.copy() for k, v in tr.params.items()}
+        neg1 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+        neg2 = O.negative_samples(tr.rng, tr.cum, tr.N, s)
+        c = [tr.train_batch(b, neg1[:, O.batch_rows(b, l)], neg2[:, O.batch_rows(b, l)])
+             for b in range(steps)]
+        out[name] = (np.array(c), tr.params)
+        del tr
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "bf16", dec, False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=graph_chunk, mfma_bf16=True)
+    ind.compile_function()
+    eng = ind.engine
+    eng.set_epoch_negatives(neg1, neg2)
+    eng.run(0, steps)
+    torch.cuda.synchronize()
+    eng.check()
+    got = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
+    out["gpu"] = (eng.costs[:steps].cpu().numpy().astype(np.float64), got)
+    ind._drop_engine()
+    return out, init
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+# Derived bf16 tolerance: the GPU trajectory must be as close to the float64 one as bf16
+# operand rounding itself allows (the emulated oracle's distance, x1.25 + 1e-4 slack for the
+# fp32 accumulation), AND much closer to the emulated oracle than either is to the exact one
+# (<= 0.25 x that distance + 1e-4): the kernels differ from the reference only by rounding
+# the R-contraction operands to bf16.  Costs alike, per batch.
+BF16_EXACT_FACTOR, BF16_EMU_FACTOR, BF16_SLACK = 1.25, 0.25, 1e-4
+
+
+def check_bf16(out, init=None, what=""):
+    ce, cm, cg = out["exact"][0], out["emu"][0], out["gpu"][0]
+    dc_emu = np.abs(cm - ce)
+    assert np.all(np.abs(cg - ce) <= BF16_EXACT_FACTOR * dc_emu + 2e-5 * np.abs(ce)), \
+        (what, cg, ce, cm)
+    assert np.all(np.abs(cg - cm) <= BF16_EMU_FACTOR * dc_emu + 2e-5 * np.abs(ce)), \
+        (what, cg, ce, cm)
+    pe, pm, pg = out["exact"][1], out["emu"][1], out["gpu"][1]
+    rep = {}
+    for k in pe:
+        d_emu, d_gpu, d_ge = _rel(pm[k], pe[k]), _rel(pg[k], pe[k]), _rel(pg[k], pm[k])
+        rep[k] = (d_emu, d_gpu, d_ge)
+        assert d_gpu <= BF16_EXACT_FACTOR * d_emu + BF16_SLACK, (what, k, rep[k])
+        assert d_ge <= BF16_EMU_FACTOR * d_emu + BF16_SLACK, (what, k, rep[k])
+        if init is not None and k in ("W", "A"):
+            untouched = np.all(pe[k] == init[k], axis=1)
+            f32 = init[k][untouched].astype(np.float32).astype(np.float64)
+            assert np.array_equal(pg[k][untouched], f32), (what, k)
+    print(what, {k: "emu %.2e gpu %.2e gpu-emu %.2e" % v for k, v in rep.items()})
+    return rep
+
+
+@pytest.mark.timeout(900)
+def test_c5_bench_size_bf16(built_lib, cuda_dev):
+    """BASELINE config 5 at the size bench.py --config c5 times: 1M synthetic triples,
+    d = 2^17, K = 100, embed 200, neg 20, l = 100, RESCAL, bf16 MFMA operands -- the row index,
+    heavy-row classes and the k_bil_rows / k_update_bil dispatch at full scale -- against the
+    float64 oracle with the derived bf16 tolerance (check_bf16) and the untouched-rows
+    property."""
+    out, init = bf16_trajectories(cuda_dev, "rescal", N=1_000_000, d=2 ** 17, m=100, r=200,
+                                  s=20, l=100, ntrue=100, steps=4)
+    check_bf16(out, init, "c5 full size")
+
+
 def _run_oracle_only(N, d, m, r, s, l, ntrue, steps, seed_data=1234):
     from rae.data import synthetic_dataset
     data, gold = synthetic_dataset(N, d, ntrue, seed=seed_data)
