@@ -215,6 +215,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--no-label-pass", action="store_true")
+    ap.add_argument("--dp-update", default="replicated", choices=["replicated", "partitioned"],
+                    help="data-parallel update (N > 1): every rank updates every row, or each "
+                         "rank the rows it owns (rows pulled from their owners each step)")
     args = ap.parse_args()
 
     import torch
@@ -237,7 +240,8 @@ def main():
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, cfg["r"], cfg["m"],
                              cfg["s"], 0.0, 0.0, "adagrad", "bench", cfg["dec"], False, True, False,
                              1.0, device=dev, world_size=ws, rank=rk, exchange=exchange,
-                             graph_chunk=args.graph_chunk, mfma_bf16=cfg.get("bf16", False))
+                             graph_chunk=args.graph_chunk, mfma_bf16=cfg.get("bf16", False),
+                             dp_update=args.dp_update)
     ind.compile_function()
     eng = ind.engine
     # per-epoch negatives: the reference's RandomState stream, CDF search on the device
@@ -263,6 +267,11 @@ def main():
     if prebuilt:
         eng.build_index(0, W + K)
         eng.check()                        # a partition overflow is reported before any step
+    if eng._dp:                            # the rows all-to-all's communicator, before capture
+        if not prebuilt:
+            eng.build_index(0, min(eng.index_window, W + K))
+        exchange.rows(eng._dp_send, eng._dp_recv)
+        torch.cuda.synchronize()
     graphed = args.graph_chunk > 1
     try:
         if graphed:                        # capture every graph the warm-up and the timed
@@ -323,7 +332,14 @@ def main():
     fev = [(_ev(), _ev()) for _ in range(n_it)]
     uev = [(_ev(), _ev()) for _ in range(n_it)]
     xev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(n_it)]
+    pev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(n_it)]
     for i in range(n_it):
+        if eng._dp:                        # partitioned update: rows pulled from their owners
+            pev[i][0].record(st)
+            assert lib.rae_dp_pack(plan, i, sp_) == 0, lib.rae_last_error()
+            exchange.rows(eng._dp_send, eng._dp_recv)
+            assert lib.rae_dp_unpack(plan, i, sp_) == 0, lib.rae_last_error()
+            pev[i][1].record(st)
         assert lib.rae_time_next(plan, fev[i][0], fev[i][1]) == 0
         assert lib.rae_step_forward(plan, i, sp_) == 0, lib.rae_last_error()
         if exchange is not None:           # the all-gather of the records (data-parallel only)
@@ -546,6 +562,9 @@ def main():
     }
     if xch_ms is not None:
         out["kernel_us"]["exchange"] = float(np.mean(xch_ms) * 1e3)
+    if eng._dp:
+        out["kernel_us"]["row_pull"] = float(np.mean([a.elapsed_time(b) for a, b in pev]) * 1e3)
+        out["config"]["dp_row_caps"] = list(eng._dp_caps)
     if rk == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, cfg, l, args.cpu_seconds)
         out["cpu_baseline"]["host_cpus"] = os.cpu_count()

@@ -185,6 +185,28 @@ int rae_step_update_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
  * rae_set_negatives(PER_CALL) + index + forward + update for `batch_index`.            */
 int rae_train_step(rae_plan* plan, int64_t batch_index, const int32_t* neg1_dev,
                    const int32_t* neg2_dev, rae_stream_t stream);
+/* --- partitioned data-parallel update (dp_update = RAE_DPUPD_PARTITIONED) ------------- *
+ * Row r of A / Ab / W is owned by rank r % world_size; rae_step_update updates the owned rows
+ * only (the dense C1 / C2 / Wb / R / C stay replicated).  Before each step's forward every
+ * rank refreshes the non-owned rows its examples read:
+ *     rae_dp_pack -> [caller: all-to-all of world_size equal blocks, send -> recv] -> rae_dp_unpack
+ * (the same cursor / absolute batch addressing as rae_step_forward / _at).  The peers' row lists
+ * are built with the row index (rae_build_index).  Parameters equal the replicated form's
+ * bitwise once the owners' rows are gathered (the caller's sync; rae/dist.py sync_rows).
+ * Requires lambda1 = lambda2 = 0.                                                          */
+/* floats of one peer block for the given row capacities (entity rows, feature rows)      */
+int64_t rae_dp_block_floats(const rae_config* cfg, int32_t cap_entities, int32_t cap_features);
+/* caller-owned send / recv buffers of world_size blocks each, and their row capacities;
+ * every list the plan builds must fit (rae_dp_list_max; a longer one sets error flag 16)   */
+int rae_set_dp_buffers(rae_plan* plan, float* send_dev, float* recv_dev, int32_t cap_entities,
+                       int32_t cap_features);
+/* longest list built since the previous call (synchronises; resets the maxima)           */
+int rae_dp_list_max(rae_plan* plan, int32_t* max_entities, int32_t* max_features);
+int rae_dp_pack(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
+int rae_dp_unpack(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
+int rae_dp_pack_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
+int rae_dp_unpack_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
+
 /* Kernel timing (bench / profiling; no reference counterpart).  Arms the NEXT
  * rae_step_forward or rae_step_update call on this plan: its kernels are launched with
  * hipExtLaunchKernelGGL so `start_event` takes the first kernel's dispatch-begin timestamp

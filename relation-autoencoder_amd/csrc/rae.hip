@@ -24,6 +24,7 @@
 #include "rae_bilinear.hpp"
 #include "rae_sp_split.hpp"
 #include "rae_common.hpp"
+#include "rae_dp.hpp"
 #include "rae_index.hpp"
 #include "rae_label.hpp"
 #include "rae_sampler.hpp"
@@ -145,6 +146,20 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_index(StepArgs a, int64_t fir
 // the update's dispatch tables of the same batches (after k_build_index)
 __global__ __launch_bounds__(RAE_BT) void k_build_tasks(StepArgs a, int64_t first) {
     build_batch_tasks<RAE_BT>(a, (first + blockIdx.x) % a.index_window);
+}
+
+// partitioned data-parallel update (rae_dp.hpp): the peers' row lists of global batches
+// [first, first + gridDim.x); blockIdx.y = peer, blockIdx.z = direction * 2 + table
+__global__ __launch_bounds__(RAE_FBT) void k_build_dplists(StepArgs a, int64_t first) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t g = first + blockIdx.x;
+    build_dp_list<RAE_FBT>(a, g, g % a.index_window, blockIdx.z >> 1, blockIdx.y, blockIdx.z & 1,
+                           smem);
+}
+template <bool PACK>
+__global__ __launch_bounds__(RAE_BT) void k_dp_move(StepArgs a) {
+    const int64_t t = (int64_t)blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    dp_move<PACK>(a, t, threadIdx.x & 63);
 }
 
 __host__ __device__ inline int n_ctiles(int dec, int r, int m) {
@@ -527,6 +542,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
+    if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
+        return fail(RAE_E_INVALID, "the partitioned data-parallel update needs lambda1 = lambda2 = 0 "
+                                   "(a regulariser makes every W row change every step)");
     if (c.batch_size < 1 || c.world_size < 1 || c.rank < 0 || c.rank >= c.world_size)
         return fail(RAE_E_INVALID, "bad batch_size/world_size/rank");
     if (c.n_examples < (int64_t)c.batch_size * c.world_size)
@@ -611,9 +629,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.RW = c.max_batch_nnz > 0 ? c.max_batch_nnz : 1;
     a.HA = index_partitions(a.RA);
     a.HW = index_partitions(a.RW);
+    a.G = c.world_size;
+    a.part = c.dp_update == RAE_DPUPD_PARTITIONED ? 1 : 0;
     {
         const int64_t nb = c.n_examples / L;
-        int64_t win = c.index_window > 0 ? c.index_window : 2048;
+        // partitioned: the peers' row lists take 2 G (LA + LW) ints per slot -> a shorter window
+        int64_t win = c.index_window > 0 ? c.index_window : (a.part ? 256 : 2048);
         if (win > nb) win = nb;
         a.index_window = win < 1 ? 1 : win;
     }
@@ -664,6 +685,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_desc = take(4ull * W_ * c.batch_size * a.dstride);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
+    // partitioned data-parallel update: list capacities are the worst cases of one rank's
+    // l examples (every entity id distinct; the largest global batch's features)
+    a.LA = a.part ? c.batch_size * NJ : 0;
+    a.LW = a.part ? a.RW : 0;
+    const size_t o_dpl = a.part ? take(4ull * W_ * dpl_slot_ints(a.G, a.LA, a.LW)) : 0;
+    const size_t o_dpc = a.part ? take(4ull * W_ * 2 * a.G * 2) : 0;
+    const size_t o_dpm = take(16);
     const bool bil = c.decoder != RAE_DEC_SP;
     a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
     // bf16 dP with LDS-staged R slices (k_bil_dp2): the C5 shape compiled exactly, other
@@ -732,6 +760,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.pfrag = a.bf16 ? reinterpret_cast<uint4*>(p->ws + o_pfr) : nullptr;
     a.err = p->d_err;
     a.cursor = p->d_cursor;
+    a.dpl = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpl) : nullptr;
+    a.dpc = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpc) : nullptr;
+    a.dpmax = reinterpret_cast<int*>(p->ws + o_dpm);
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -792,6 +823,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         }
         (void)hipFuncSetAttribute((const void*)k_build_index,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
+        (void)hipFuncSetAttribute((const void*)k_build_dplists,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(4 * RAE_DPL_KEYS + 4 * 32));
     }
     *out = p;
     return RAE_OK;
@@ -979,6 +1013,11 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, p->args, first);
     HIPCHK(hipGetLastError());
+    if (p->args.part) {
+        hipLaunchKernelGGL(k_build_dplists, dim3((unsigned)count, p->args.G, 4), dim3(RAE_FBT),
+                           4 * RAE_DPL_KEYS + 4 * 32, st, p->args, first);
+        HIPCHK(hipGetLastError());
+    }
     return RAE_OK;
 }
 
@@ -1012,6 +1051,72 @@ extern "C" int rae_step_update_at(rae_plan* p, int64_t batch, rae_stream_t strea
     if (!p) return fail(RAE_E_INVALID, "null plan");
     if (int rc = check_batch(p, batch)) return rc;
     return launch_update(p, nullptr, batch, (hipStream_t)stream);
+}
+
+// ---- partitioned data-parallel update (rae_dp.hpp) ----
+extern "C" int64_t rae_dp_block_floats(const rae_config* cfg, int32_t cap_entities,
+                                       int32_t cap_features) {
+    if (!cfg || cap_entities < 0 || cap_features < 0) return -1;
+    return dp_block_floats(cfg->embed, cfg->relations, cap_entities, cap_features);
+}
+extern "C" int rae_set_dp_buffers(rae_plan* p, float* send, float* recv, int32_t cap_entities,
+                                  int32_t cap_features) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (!p->args.part) return fail(RAE_E_STATE, "the plan's data-parallel update is not partitioned");
+    if (!send || !recv || cap_entities < 0 || cap_features < 0 || cap_entities > p->args.LA ||
+        cap_features > p->args.LW)
+        return fail(RAE_E_INVALID, "bad row-exchange buffers / capacities");
+    StepArgs& a = p->args;
+    a.dsend = send;
+    a.drecv = recv;
+    a.capA = cap_entities;
+    a.capW = cap_features;
+    a.dblk = dp_block_floats(a.r, a.m, a.capA, a.capW);
+    return RAE_OK;
+}
+extern "C" int rae_dp_list_max(rae_plan* p, int32_t* max_entities, int32_t* max_features) {
+    if (!p || !max_entities || !max_features) return fail(RAE_E_INVALID, "null argument");
+    int v[2] = {0, 0};
+    HIPCHK(hipMemcpy(v, p->args.dpmax, sizeof(v), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(p->args.dpmax, 0, sizeof(v)));
+    *max_entities = v[0];
+    *max_features = v[1];
+    return RAE_OK;
+}
+static int launch_dp_move(rae_plan* p, bool pack, const int64_t* cursor, int64_t off, hipStream_t st) {
+    const StepArgs& a0 = p->args;
+    if (!a0.part) return fail(RAE_E_STATE, "the plan's data-parallel update is not partitioned");
+    if (a0.G == 1) return RAE_OK;                   // every row is this rank's
+    if (!a0.dsend || !a0.drecv) return fail(RAE_E_STATE, "row-exchange buffers not set");
+    StepArgs a = a0;
+    a.cursor = cursor;
+    a.step_offset = off;
+    const int64_t waves = (int64_t)a.G * (a.capA + a.capW);
+    if (waves == 0) return RAE_OK;
+    const dim3 gr((unsigned)((waves + RAE_NWAVE - 1) / RAE_NWAVE));
+    if (pack) RAE_LAUNCH(p, k_dp_move<true>, gr, dim3(RAE_BT), 0, st, a);
+    else RAE_LAUNCH(p, k_dp_move<false>, gr, dim3(RAE_BT), 0, st, a);
+    p->t_start = p->t_stop = nullptr;
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
+extern "C" int rae_dp_pack(rae_plan* p, int64_t off, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    return launch_dp_move(p, true, p->d_cursor, off, (hipStream_t)stream);
+}
+extern "C" int rae_dp_unpack(rae_plan* p, int64_t off, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    return launch_dp_move(p, false, p->d_cursor, off, (hipStream_t)stream);
+}
+extern "C" int rae_dp_pack_at(rae_plan* p, int64_t batch, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (int rc = check_batch(p, batch)) return rc;
+    return launch_dp_move(p, true, nullptr, batch, (hipStream_t)stream);
+}
+extern "C" int rae_dp_unpack_at(rae_plan* p, int64_t batch, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (int rc = check_batch(p, batch)) return rc;
+    return launch_dp_move(p, false, nullptr, batch, (hipStream_t)stream);
 }
 
 extern "C" int rae_time_next(rae_plan* p, void* start, void* stop) {
@@ -1074,7 +1179,9 @@ extern "C" int rae_check(rae_plan* p) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     int e = 0;
     HIPCHK(hipMemcpy(&e, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail(RAE_E_OVERFLOW, "row-index partition overflowed its LDS capacity (flags=" +
+    if (e) return fail(RAE_E_OVERFLOW, std::string(e & 8 ? "a data-parallel row list overflowed "
+                                                         "its capacity; " : "") +
+                                           "row-index partition overflow (flags=" +
                                            std::to_string(e) + ")");
     return RAE_OK;
 }

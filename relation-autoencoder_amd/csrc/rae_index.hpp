@@ -135,7 +135,9 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
                 }
                 rec = ((unsigned)lo << a.posbits) | (unsigned)(idx - (sptr[lo] - P0));
             }
-            if (row % H == h) {
+            // partitioned data-parallel update: this rank's update visits only the rows it
+            // owns (rae_dp.hpp)
+            if (row % H == h && (!a.part || row % a.G == a.rank)) {
                 const int sl = atomicAdd(&sint[0], 1);
                 if (sl < RAE_KCAP) keys[sl] = ((unsigned long long)(unsigned)row << 32) | rec;
             }

@@ -121,6 +121,16 @@ struct StepArgs {
     int nregW;           // number of dense-W block partial slots
     float* base_cost;    // cost before the regulariser (reg_on only)
     int* err;            // device error word
+    // row-owner partitioned data-parallel update (rae_dp.hpp): G ranks, rows owned row % G
+    int G, part;         // world size; 1 when dp_update is partitioned
+    int32_t* dpl;        // per slot: the peers' row lists (dpl_slot_ints each)
+    int32_t* dpc;        // per slot: their lengths [dir][peer][table]
+    int LA, LW;          // list capacities (entity rows, feature rows)
+    float* dsend;        // caller's all-to-all buffers: G peer blocks of dblk floats
+    float* drecv;
+    int capA, capW;      // rows per peer block (set with the buffers; <= LA / LW)
+    int64_t dblk;
+    int* dpmax;          // longest list built since the last rae_dp_list_max [entity, feature]
     unsigned long long* stamps;   // diagnostic build only (RAE_STAMPS): phase timestamps
 };
 

@@ -74,6 +74,8 @@ EXPORTS = (
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
     "rae_stream_copy", "rae_mfma_probe", "rae_plan_forms",
+    "rae_dp_block_floats", "rae_set_dp_buffers", "rae_dp_list_max", "rae_dp_pack",
+    "rae_dp_unpack", "rae_dp_pack_at", "rae_dp_unpack_at",
 )
 
 
@@ -147,6 +149,15 @@ def load(path: str | None = None):
     lib.rae_plan_create.argtypes = [C.POINTER(RaeConfig), C.POINTER(RaeBuffers), C.POINTER(_P)]
     lib.rae_plan_destroy.argtypes = [_P]
     lib.rae_plan_forms.argtypes = [_P, C.POINTER(RaeConfig)]
+    lib.rae_dp_block_floats.argtypes = [C.POINTER(RaeConfig), C.c_int32, C.c_int32]
+    lib.rae_dp_block_floats.restype = C.c_int64
+    lib.rae_set_dp_buffers.argtypes = [_P, _P, _P, C.c_int32, C.c_int32]
+    lib.rae_dp_list_max.argtypes = [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    for fn in ("rae_dp_pack", "rae_dp_unpack", "rae_dp_pack_at", "rae_dp_unpack_at"):
+        getattr(lib, fn).argtypes = [_P, C.c_int64, _P]
+        getattr(lib, fn).restype = C.c_int
+    for fn in ("rae_set_dp_buffers", "rae_dp_list_max"):
+        getattr(lib, fn).restype = C.c_int
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]
     lib.rae_advance_cursor.argtypes = [_P, C.c_int64, _P]

@@ -10,6 +10,11 @@ rank then runs the identical deterministic update, so the replicas stay bit-iden
 This is the same gradient as a dense all-reduce of dW (d,m), dA (n,r), dAb (n), dC (r,m)
 summed over ranks -- at 0.52 MB per rank per step instead of >200 MB for the dense
 gradients at the headline shape.
+
+Partitioned update (dp_update="partitioned", include/rae.h RAE_DPUPD_PARTITIONED): rank k
+updates only the A / Ab / W rows it owns (row % G == k) and, before each forward, every owner
+sends each peer the rows that peer's examples read (Exchange.rows, an all-to-all); replicas
+differ in rows nobody read recently until Exchange.sync_rows gathers them.
 """
 from __future__ import annotations
 
@@ -41,28 +46,86 @@ def init(backend: str | None = None):
     return ws, rk, lr
 
 
-def make_exchange(world_size: int, rank: int, group=None):
-    """All-gather of the exchange buffer: rank k's slice is rows [k*l, (k+1)*l).
+class Exchange:
+    """The collectives of one data-parallel plan (one process per GPU).
 
-    RCCL ("nccl" backend) gathers in place in HBM, stream-ordered, so it can sit inside a
-    captured HIP graph.  The gloo backend (CPU tests; several ranks sharing one GPU) has no
-    device path: the buffer is staged through host memory, which synchronises the stream, so
-    that mode runs eagerly (graph_chunk=1)."""
-    if world_size == 1:
-        return None
+    exchange(buf)            in-place all-gather of the per-example records: rank k's slice is
+                             rows [k*l, (k+1)*l) of the global batch.
+    exchange.rows(send, recv)
+                             all-to-all of equal peer blocks (partitioned update: owners send
+                             the rows each peer's next forward reads, include/rae.h rae_dp_*).
+    exchange.max_int(v)      max over ranks (the row-list capacities every rank must agree on).
+    exchange.sync_rows(ts)   gather, for every tensor, row x from its owner x % G (replicas of
+                             the partitioned update made identical: labelling, checkpoints).
 
-    def exchange(buf: torch.Tensor):
-        n = buf.numel() // world_size
-        if buf.is_cuda and dist.get_backend(group) != "nccl":
+    RCCL ("nccl" backend) moves the device buffers in place, stream-ordered, so the records and
+    rows collectives can sit inside a captured HIP graph.  The gloo backend (CPU tests; several
+    ranks sharing one GPU) has no device path: buffers are staged through host memory, which
+    synchronises the stream, so that mode runs eagerly (graph_chunk=1)."""
+
+    def __init__(self, world_size: int, rank: int, group=None):
+        self.world_size = world_size
+        self.rank = rank
+        self.group = group
+
+    def _staged(self, t):
+        return t.is_cuda and dist.get_backend(self.group) != "nccl"
+
+    def __call__(self, buf: torch.Tensor):
+        n = buf.numel() // self.world_size
+        rk = self.rank
+        if self._staged(buf):
             host = buf.cpu()
-            dist.all_gather_into_tensor(host, host[rank * n:(rank + 1) * n].clone(), group=group)
+            dist.all_gather_into_tensor(host, host[rk * n:(rk + 1) * n].clone(), group=self.group)
             buf.copy_(host)
         elif not buf.is_cuda:
-            dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n].clone(), group=group)
+            dist.all_gather_into_tensor(buf, buf[rk * n:(rk + 1) * n].clone(), group=self.group)
         else:
-            dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n], group=group)
+            dist.all_gather_into_tensor(buf, buf[rk * n:(rk + 1) * n], group=self.group)
 
-    return exchange
+    def rows(self, send: torch.Tensor, recv: torch.Tensor):
+        if self._staged(send):
+            hs = send.cpu()
+            hr = torch.empty_like(hs)
+            dist.all_to_all_single(hr, hs, group=self.group)
+            recv.copy_(hr)
+        else:
+            dist.all_to_all_single(recv, send, group=self.group)
+
+    def max_int(self, v: int) -> int:
+        dev = torch.device("cuda", torch.cuda.current_device()) if \
+            dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def sync_rows(self, tensors):
+        """Row x of every tensor (dim 0) is current on rank x % G: gather every row from its
+        owner, so all replicas hold identical tensors (bitwise copies, no arithmetic)."""
+        G, rk = self.world_size, self.rank
+        for t in tensors:
+            if t is None:
+                continue
+            n = t.shape[0]
+            per = -(-n // G)
+            mine = t[rk::G]
+            buf = torch.zeros((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            buf[:mine.shape[0]] = mine
+            staged = self._staged(t)
+            src = buf.cpu() if staged else buf
+            out = torch.empty((G * per,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+            dist.all_gather_into_tensor(out, src, group=self.group)
+            out = out.to(t.device)
+            for k in range(G):
+                cnt = len(range(k, n, G))
+                t[k::G] = out[k * per:k * per + cnt]
+
+
+def make_exchange(world_size: int, rank: int, group=None):
+    """The Exchange of a world_size > 1 data-parallel run (None for one rank)."""
+    if world_size == 1:
+        return None
+    return Exchange(world_size, rank, group)
 
 
 def warm_up(exchange, buf):

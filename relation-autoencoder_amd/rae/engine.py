@@ -69,7 +69,7 @@ class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
                  index_window=0, device=None, mfma_bf16=False, kernel_forms=None,
-                 graph_absolute=False):
+                 graph_absolute=False, dp_update="replicated"):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -115,6 +115,13 @@ class TrainEngine:
         # kernel forms (include/rae.h RAE_SPFWD_* ...): {"sp_forward": "split", ...}; the
         # plan picks for the shape when a form is not named
         self.kernel_forms = dict(kernel_forms or {})
+        if dp_update not in _lib.KERNEL_FORMS["dp_update"]:
+            raise ValueError(f"dp_update must be one of {sorted(_lib.KERNEL_FORMS['dp_update'])}")
+        self.kernel_forms.setdefault("dp_update", dp_update)
+        # partitioned update with peers: rows are pulled from their owners before each forward
+        self._dp = self.kernel_forms["dp_update"] == "partitioned" and self.world_size > 1
+        if self._dp and exchange is None:
+            raise ValueError("the partitioned data-parallel update needs the ranks' Exchange")
         for key, val in self.kernel_forms.items():
             if key not in _lib.KERNEL_FORMS or val not in _lib.KERNEL_FORMS[key]:
                 raise ValueError(f"unknown kernel form {key}={val!r}")
@@ -144,6 +151,12 @@ class TrainEngine:
         bufs.exchange, bufs.costs = p(self.exchange_buf), p(self.costs)
         self._bufs = bufs
         self._keep = (named, acc, R3)
+        self._named, self._acc = named, acc
+        # row-exchange buffers of the partitioned update (sized from the row lists: _dp_caps)
+        self._dp_caps = None
+        self._dp_send = self._dp_recv = None
+        self._stale = set()          # partitioned: {"params", "acc"} not gathered since a run
+        self._dp_cap_max = (self.l * (2 + 2 * self.s), max(int(mbn), 1))   # rae.hip LA / LW
         handle = C.c_void_p()
         _lib.check(self.lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(handle)),
                    "rae_plan_create")
@@ -167,6 +180,44 @@ class TrainEngine:
         # this engine (set_cursor / run); a caller driving the plan directly calls
         # cursor_moved() afterwards.
         self._cursor_at = None
+
+    # ------------------------------------------------------------------ partitioned update
+    def _dp_caps_check(self):
+        """After a row-index build: the longest peer row list of the batches just built,
+        agreed over the ranks; (re)size the all-to-all blocks when a list would not fit (a
+        resize drops the captured graphs, which hold the old buffers)."""
+        ma, mw = C.c_int32(), C.c_int32()
+        _lib.check(self.lib.rae_dp_list_max(self.plan, C.byref(ma), C.byref(mw)), "rae_dp_list_max")
+        need_a = self.exchange.max_int(ma.value)
+        need_w = self.exchange.max_int(mw.value)
+        ca, cw = self._dp_caps or (0, 0)
+        if self._dp_send is not None and need_a <= ca and need_w <= cw:
+            return
+        # headroom: later windows' lists vary by a few percent around the first's
+        ca = min(max(ca, int(need_a * 1.25) + 16), self._dp_cap_max[0])
+        cw = min(max(cw, int(need_w * 1.25) + 16), self._dp_cap_max[1])
+        blk = int(self.lib.rae_dp_block_floats(C.byref(self.cfg), ca, cw))
+        self._dp_send = torch.zeros(self.world_size * blk, dtype=torch.float32, device=self.device)
+        self._dp_recv = torch.zeros_like(self._dp_send)
+        _lib.check(self.lib.rae_set_dp_buffers(self.plan, C.c_void_p(self._dp_send.data_ptr()),
+                                               C.c_void_p(self._dp_recv.data_ptr()), ca, cw),
+                   "rae_set_dp_buffers")
+        self._dp_caps = (ca, cw)
+        self._graphs.clear()
+
+    def sync_replicas(self, accumulators: bool = True):
+        """Partitioned update: gather every A / Ab / W row (and AdaGrad accumulator) from its
+        owner, so every rank holds the whole current model (labelling, checkpoints, tests).
+        No-op for the replicated update (replicas are identical after every step)."""
+        if not self._dp:
+            return
+        torch.cuda.synchronize(self.device)
+        ts = [self._named["W"], self._named["A"], self._named["Ab"]]
+        self._stale.discard("params")
+        if accumulators and self._acc:
+            ts += [self._acc.get("W"), self._acc.get("A"), self._acc.get("Ab")]
+            self._stale.discard("acc")
+        self.exchange.sync_rows(ts)
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -289,6 +340,17 @@ class TrainEngine:
         given) at absolute batches first, first+1, ... (the cursor is not touched: every
         cursor-driven run sets it first)."""
         for i in range(count):
+            if self._dp:                     # pull the rows this step's examples read
+                if first is None:
+                    _lib.check(self.lib.rae_dp_pack(self.plan, i, st), "rae_dp_pack")
+                else:
+                    _lib.check(self.lib.rae_dp_pack_at(self.plan, first + i, st), "rae_dp_pack_at")
+                self.exchange.rows(self._dp_send, self._dp_recv)
+                if first is None:
+                    _lib.check(self.lib.rae_dp_unpack(self.plan, i, st), "rae_dp_unpack")
+                else:
+                    _lib.check(self.lib.rae_dp_unpack_at(self.plan, first + i, st),
+                               "rae_dp_unpack_at")
             if first is None:
                 _lib.check(self.lib.rae_step_forward(self.plan, i, st), "rae_step_forward")
             else:
@@ -386,6 +448,8 @@ class TrainEngine:
         """Row index of batches [first_batch, first_batch+count) (one window at most)."""
         _lib.check(self.lib.rae_build_index(self.plan, int(first_batch), int(count), self._stream()),
                    "rae_build_index")
+        if self._dp:
+            self._dp_caps_check()
 
     def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True,
             last_advance: bool = True):
@@ -396,13 +460,17 @@ class TrainEngine:
         every step runs inside a replayed HIP graph: graph_chunk-step graphs and one graph
         per window remainder (last_advance: see _cursor_replays)."""
         self._ensure_epoch_mode()
+        if self._dp:
+            self._stale.update(("params", "acc"))
         replays = self._cursor_replays(first_batch, count, last_advance)
         for wi, (b, n) in enumerate(self.windows(first_batch, count)):
             if index:
                 _lib.check(self.lib.rae_build_index(self.plan, b, n, self._stream()),
                            "rae_build_index")
-                if self._index_partitioned:
+                if self._index_partitioned or self._dp:
                     self.check()
+                if self._dp:
+                    self._dp_caps_check()
             if graph and self.graph_chunk > 1 and self.graph_absolute:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
@@ -423,6 +491,8 @@ class TrainEngine:
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):
         """labels (int64) and probs (fp32) of rows [row0, row0+nrows) of a split with the
         current W/Wb (RelationClassifier.py:39-48)."""
+        if "params" in self._stale:          # partitioned update: gather W from its owners
+            self.sync_replicas(accumulators=False)
         lab = torch.empty(nrows, dtype=torch.int64, device=self.device)
         pr = torch.empty((nrows, self.m), dtype=torch.float32, device=self.device) if probs else None
         W, Wb = self.model.params[0], self.model.params[1]

@@ -54,7 +54,7 @@ class ReconstructInducer:
                  model_name, decoder_model, external_embeddings, extended_regularizer,
                  frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
                  graph_chunk=64, neg_sampler="device", neg_seed=0, mfma_bf16=False,
-                 kernel_forms=None):
+                 kernel_forms=None, dp_update="replicated"):
         self.data = data
         self.goldStandard = gold_standard
         self.rng = rng
@@ -84,6 +84,7 @@ class ReconstructInducer:
         self.neg_seed = int(neg_seed)
         self.mfma_bf16 = bool(mfma_bf16)   # RESCAL / hybrid: bf16 MFMA operands (config 5)
         self.kernel_forms = dict(kernel_forms or {})   # engine.TrainEngine kernel_forms
+        self.dp_update = dp_update         # "replicated" | "partitioned" (rae/dist.py)
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
                         f"_embedsize{embed_size}_l1{lambda1}_l2{lambda2}_opt{optimization}"
@@ -146,7 +147,8 @@ class ReconstructInducer:
                                   lambda2=self.lambdaL2, world_size=self.world_size,
                                   rank=self.rank, exchange=self.exchange,
                                   graph_chunk=self.graph_chunk, device=self.device,
-                                  mfma_bf16=self.mfma_bf16, kernel_forms=self.kernel_forms)
+                                  mfma_bf16=self.mfma_bf16, kernel_forms=self.kernel_forms,
+                                  dp_update=self.dp_update)
         self.func["train"] = _TrainFunction(self.engine)
         for key in self.data.generate_split_keys():
             ds = self.engine.split if key == "train" else DeviceSplit(self.data.split[key], self.device)
@@ -271,6 +273,8 @@ class ReconstructInducer:
         """Parameters + AdaGrad accumulators + RNG state + epoch cursor (the reference's
         save() keeps only the parameters and loses the accumulators and the RNG position,
         OieInduction.py:110-116, so a reloaded model cannot continue the same run)."""
+        if self.engine is not None:         # partitioned update: rows from their owners
+            self.engine.sync_replicas(accumulators=True)
         sd = {"params": {k: v.detach().cpu() for k, v in self.modelFunc.named_params().items()},
               "rng": self.rng.get_state(), "epoch": self.cur_epoch,
               "train_errors": list(self.train_errors)}

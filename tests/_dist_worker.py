@@ -13,7 +13,10 @@ MODE
   gpu        the real HIP path with world_size 2: both ranks share cuda:0, the exchange
              records go through gloo (host-staged), eager steps.  Each rank saves its
              params and per-batch costs.
-  gpu_c3     the same at BASELINE config 3's full size with global batch L = 800 (2 x 400).
+  gpu_c3     the same at BASELINE config 3's full size with global batch L = 800 (2 x 400);
+             argument 3: the data-parallel update ("replicated" | "partitioned").
+  oracle_part  the row-owner partitioned update's protocol on the float64 oracle.
+  rows       rae.dist.Exchange.rows / sync_rows / max_int over gloo.
 """
 import os
 import sys
@@ -86,7 +89,99 @@ def run_oracle(out, decoder, lambda1=0.0):
     np.savez(os.path.join(out, f"oracle_{decoder}_{rk}.npz"), costs=np.array(costs), **p)
 
 
-def run_gpu(out, decoder):
+def _reads(sp_, n1, n2, rows):
+    """Entity rows (e1, e2, negatives) and feature rows the examples `rows` read."""
+    ents = np.unique(np.concatenate([sp_.args1[rows], sp_.args2[rows], n1[:, rows].ravel(),
+                                     n2[:, rows].ravel()]))
+    return ents, np.unique(sp_.xFeats[rows].indices)
+
+
+def run_oracle_part(out, decoder):
+    """The row-owner partitioned update (include/rae.h RAE_DPUPD_PARTITIONED) on the float64
+    oracle: every rank keeps a replica, only row x's owner (x % G) applies x's A / Ab / W
+    update, and before each forward every owner sends each peer the rows that peer's examples
+    read.  Non-owned rows nobody pulled go stale -- if the pull lists missed a row, a forward
+    would read a stale value and the run would leave the global-batch trajectory.  At the end
+    the owners' rows are gathered (Exchange.sync_rows)."""
+    import rae_oracle as O
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    data, _ = _dataset()
+    sp_ = data.split["train"]
+    m, r, s, l = DP_SHAPE["m"], DP_SHAPE["r"], DP_SHAPE["s"], DP_SHAPE["l"]
+    L = ws * l
+    N = sp_.xFeats.shape[0]
+    rng = np.random.RandomState(2)
+    p = O.init_params(rng, decoder, data.get_dimensionality(), m, data.get_arg_voc_size(), r)
+    acc = {k: np.zeros_like(v) for k, v in p.items()}
+    own = {"A": np.arange(p["A"].shape[0]) % ws == rk, "W": np.arange(p["W"].shape[0]) % ws == rk}
+    own["Ab"] = own["A"]
+    D = 4 * L + 2 * L * s
+    costs = []
+    for ep in range(DP_SHAPE["epochs"]):
+        n1 = O.negative_samples(rng, data.negSamplingCum, N, s)
+        n2 = O.negative_samples(rng, data.negSamplingCum, N, s)
+        for b in range(N // L):
+            # pull: owner -> reader, exactly the rows each peer reads and this rank owns
+            send = {}
+            for j in range(ws):
+                if j != rk:
+                    e, f = _reads(sp_, n1, n2, slice(b * L + j * l, b * L + (j + 1) * l))
+                    e, f = e[e % ws == rk], f[f % ws == rk]
+                    send[j] = (e, p["A"][e].copy(), p["Ab"][e].copy(), f, p["W"][f].copy())
+            box = [None] * ws
+            dist.all_gather_object(box, send)
+            for k in range(ws):
+                if k != rk:
+                    e, a_, ab_, f, w_ = box[k][rk]
+                    p["A"][e], p["Ab"][e], p["W"][f] = a_, ab_, w_
+            rows = slice(b * L + rk * l, b * L + (rk + 1) * l)
+            res = O.train_step_grads(decoder, p, sp_.xFeats[rows], sp_.args1[rows],
+                                     sp_.args2[rows], n1[:, rows], n2[:, rows], alpha=1.0,
+                                     denom=D)
+            names = list(res.grads)
+            flat = torch.from_numpy(np.concatenate([res.grads[k].ravel() for k in names] +
+                                                   [np.array([res.cost])]))
+            dist.all_reduce(flat)                # == the records' contributions, summed
+            flat = flat.numpy()
+            o = 0
+            for k in names:
+                g = flat[o:o + res.grads[k].size].reshape(res.grads[k].shape)
+                o += res.grads[k].size
+                msk = own.get(k)                 # rows: the owner only; dense: every rank
+                if msk is None:
+                    O.adagrad_apply({k: p[k]}, {k: acc[k]}, {k: g}, 0.1)
+                else:
+                    sub_p, sub_a = {k: p[k][msk]}, {k: acc[k][msk]}
+                    O.adagrad_apply(sub_p, sub_a, {k: g[msk]}, 0.1)
+                    p[k][msk], acc[k][msk] = sub_p[k], sub_a[k]
+            costs.append(flat[o])
+    # gather every row from its owner (the replicas now identical)
+    box = [None] * ws
+    dist.all_gather_object(box, {k: p[k][own[k]] for k in ("A", "Ab", "W")})
+    for k in ("A", "Ab", "W"):
+        for j in range(ws):
+            p[k][np.arange(p[k].shape[0]) % ws == j] = box[j][k]
+    np.savez(os.path.join(out, f"oraclepart_{decoder}_{rk}.npz"), costs=np.array(costs), **p)
+
+
+def run_sync_rows(out):
+    """Exchange.rows (all-to-all of equal blocks) and Exchange.sync_rows over gloo."""
+    from rae import dist as rdist
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    ex = rdist.make_exchange(ws, rk)
+    send = torch.arange(ws * 3, dtype=torch.float32) + 1000 * rk     # block j -> rank j
+    recv = torch.full_like(send, -1.0)
+    ex.rows(send, recv)
+    t2 = torch.full((11, 3), -1.0)
+    t2[rk::ws] = torch.arange(11, dtype=torch.float32)[rk::ws, None] * 10 + rk
+    t1 = torch.full((7,), -1.0)
+    t1[rk::ws] = torch.arange(7, dtype=torch.float32)[rk::ws] + 0.5
+    ex.sync_rows([t2, t1])
+    assert ex.max_int(rk * 3 + 1) == (ws - 1) * 3 + 1
+    np.savez(os.path.join(out, f"rows_{rk}.npz"), recv=recv.numpy(), t2=t2.numpy(), t1=t1.numpy())
+
+
+def run_gpu(out, decoder, dp_update="replicated"):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -97,14 +192,16 @@ def run_gpu(out, decoder):
     ex = rdist.make_exchange(ws, rk)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), DP_SHAPE["epochs"], 0.1, l, r,
                              m, s, 0.0, 0.0, "adagrad", "dp", decoder, False, True, False, 1.0,
-                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1)
+                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
+                             dp_update=dp_update)
     ind.learn(verbose=False)
+    ind.engine.sync_replicas()
     params = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
-    np.savez(os.path.join(out, f"gpu_{decoder}_{rk}.npz"),
+    np.savez(os.path.join(out, f"gpu_{dp_update}_{decoder}_{rk}.npz"),
              costs=np.concatenate(ind.epoch_costs), **params)
 
 
-def run_gpu_c3(out, steps=3):
+def run_gpu_c3(out, steps=3, dp_update="replicated"):
     """BASELINE config 3 at full size (1M triples) with the global batch of 8 ranks at l=100,
     L = 800, split over 2 ranks of l = 400: the first `steps` batches of an epoch, negatives
     from the reference's RandomState stream (device CDF search)."""
@@ -118,13 +215,15 @@ def run_gpu_c3(out, steps=3):
     ex = rdist.make_exchange(ws, rk)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 800 // ws, 200, 100,
                              20, 0.0, 0.0, "adagrad", "dp800", "sp", False, True, False, 1.0,
-                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1)
+                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
+                             dp_update=dp_update)
     ind.compile_function()
     eng = ind.engine
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
     eng.run(0, steps)
     torch.cuda.synchronize()
     eng.check()
+    eng.sync_replicas()
     np.save(os.path.join(out, f"c3_costs_{rk}.npy"), eng.costs[:steps].cpu().numpy())
     for k, v in ind.modelFunc.named_params().items():
         np.save(os.path.join(out, f"c3_{k}_{rk}.npy"), v.detach().cpu().numpy())
@@ -140,10 +239,14 @@ def main():
             run_exchange(out)
         elif mode == "oracle":
             run_oracle(out, dec, lambda1=float(sys.argv[4]) if len(sys.argv) > 4 else 0.0)
+        elif mode == "oracle_part":
+            run_oracle_part(out, dec)
+        elif mode == "rows":
+            run_sync_rows(out)
         elif mode == "gpu":
-            run_gpu(out, dec)
+            run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated")
         elif mode == "gpu_c3":
-            run_gpu_c3(out)
+            run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated")
         else:
             raise SystemExit(f"unknown mode {mode}")
         dist.barrier()

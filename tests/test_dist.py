@@ -70,16 +70,71 @@ def test_partition_equals_global_batch(tmp_path, decoder, lambda1, ws):
         np.testing.assert_allclose(rs[0][k], v, rtol=1e-9, atol=1e-11, err_msg=k)
 
 
+@pytest.mark.parametrize("ws", [2, 4])
+def test_row_exchange_and_sync_gloo(tmp_path, ws):
+    """Exchange.rows delivers block k of rank j's send buffer to block j of rank k's receive
+    buffer; Exchange.sync_rows gives every rank row x from rank x % G."""
+    _launch(["rows", str(tmp_path)], nproc=ws)
+    t2 = np.arange(11, dtype=np.float32)[:, None] * 10 + (np.arange(11) % ws)[:, None]
+    t2 = np.repeat(t2, 3, axis=1)
+    t1 = np.arange(7, dtype=np.float32) + 0.5
+    for k in range(ws):
+        z = np.load(tmp_path / f"rows_{k}.npz")
+        want = np.concatenate([np.arange(3 * k, 3 * k + 3, dtype=np.float32) + 1000 * j
+                               for j in range(ws)])
+        np.testing.assert_array_equal(z["recv"], want)
+        np.testing.assert_array_equal(z["t2"], t2)
+        np.testing.assert_array_equal(z["t1"], t1)
+
+
+@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4),
+                                        ("rescal+sp", 4), ("sp", 8)])
+def test_partitioned_update_equals_global_batch(tmp_path, decoder, ws):
+    """The row-owner partitioned update's protocol (owners update their rows, readers pull
+    exactly the rows their examples read before each forward) on the float64 oracle == the
+    single-process oracle at the global batch; replicas identical after the final gather."""
+    _launch(["oracle_part", str(tmp_path), decoder], nproc=ws)
+    tr, costs = _single_process_oracle(decoder, ws=ws)
+    rs = [np.load(tmp_path / f"oraclepart_{decoder}_{k}.npz") for k in range(ws)]
+    np.testing.assert_allclose(rs[0]["costs"], costs, rtol=1e-10, atol=1e-12)
+    for k, v in tr.params.items():
+        for rk in rs[1:]:
+            np.testing.assert_array_equal(rs[0][k], rk[k])
+        np.testing.assert_allclose(rs[0][k], v, rtol=1e-9, atol=1e-11, err_msg=k)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4),
                                         ("sp", 8), ("rescal+sp", 8)])
 def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws):
     _launch(["gpu", str(tmp_path), decoder], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
-    gs = [np.load(tmp_path / f"gpu_{decoder}_{k}.npz") for k in range(ws)]
+    gs = [np.load(tmp_path / f"gpu_replicated_{decoder}_{k}.npz") for k in range(ws)]
     np.testing.assert_allclose(gs[0]["costs"], costs, rtol=2e-5, atol=2e-5)
     for k, v in tr.params.items():
         for gk in gs[1:]:
             np.testing.assert_array_equal(gs[0][k], gk[k])    # bit-identical replicas
         err = np.abs(gs[0][k] - v)
+        assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal+sp", 2), ("sp", 4), ("rescal", 4),
+                                        ("sp", 8)])
+def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws):
+    """The HIP path with the row-owner partitioned update (k_build_dplists, k_dp_move, the
+    owned-rows row index) on `ws` ranks sharing the GPU: == the oracle at the global batch,
+    and bit-identical to the replicated update's parameters and costs."""
+    _launch(["gpu", str(tmp_path), decoder, "partitioned"], nproc=ws)
+    _launch(["gpu", str(tmp_path), decoder, "replicated"], nproc=ws)
+    tr, costs = _single_process_oracle(decoder, ws=ws)
+    gp = [np.load(tmp_path / f"gpu_partitioned_{decoder}_{k}.npz") for k in range(ws)]
+    gr = np.load(tmp_path / f"gpu_replicated_{decoder}_0.npz")
+    np.testing.assert_array_equal(gp[0]["costs"], gr["costs"])
+    np.testing.assert_allclose(gp[0]["costs"], costs, rtol=2e-5, atol=2e-5)
+    for k, v in tr.params.items():
+        for g in gp[1:]:
+            np.testing.assert_array_equal(gp[0][k], g[k])
+        np.testing.assert_array_equal(gp[0][k], gr[k])
+        err = np.abs(gp[0][k] - v)
         assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"

@@ -298,12 +298,15 @@ def test_c4_full_size(built_lib, cuda_dev):
     assert np.array_equal(named["A"][ue_t].cpu().numpy(), A0)
 
 
-def test_c3_global_batch_800_two_ranks(built_lib, cuda_dev, tmp_path):
+@pytest.mark.parametrize("dp_update", ["replicated", "partitioned"])
+def test_c3_global_batch_800_two_ranks(built_lib, cuda_dev, tmp_path, dp_update):
     """The data-parallel path itself at C3's full size: 2 ranks x l = 400 (the global batch of
-    8 ranks at l = 100), records all-gathered between the forward and the update, against the
-    float64 oracle at the global batch L = 800; the two replicas bit-identical."""
+    8 ranks at l = 100), records all-gathered between the forward and the update (replicated:
+    every rank updates every row; partitioned: each rank its own rows, rows pulled from their
+    owners before each forward), against the float64 oracle at the global batch L = 800; the
+    two replicas bit-identical (partitioned: after the final gather)."""
     import test_dist
-    test_dist._launch(["gpu_c3", str(tmp_path)], timeout=600)
+    test_dist._launch(["gpu_c3", str(tmp_path), dp_update], timeout=600)
     want_c, _, want_p, _, init = _run_oracle_only(N=1_000_000, d=2 ** 17, m=100, r=200, s=20,
                                                   l=800, ntrue=100, steps=3)
     c0 = np.load(tmp_path / "c3_costs_0.npy").astype(np.float64)

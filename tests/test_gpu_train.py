@@ -581,6 +581,24 @@ def test_degenerate_shapes_vs_oracle(built_lib, cuda_dev, dec, shape):
     _assert_params_close(_params(ind), tr.params, "tiny")
 
 
+@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
+def test_bilinear_many_relations_vs_oracle(built_lib, cuda_dev, dec):
+    """K = 400 relations on a bilinear decoder (fp32): an 8 x 16 x K block of R no longer fits
+    in LDS (512 K bytes > 160 KiB above K = 320), so the M-tile passes read R from L2
+    (k_bil_mt<false, true>); float4 rows (K multiple of 4) and the R-row update's non-LDS path."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = 400, 24, 3, 40
+    data, gold = synthetic_dataset(120, 600, 6, seed=31)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "bigk", dec, False, True, False, 1.0, device=cuda_dev,
+                             graph_chunk=2)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, 1, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "bigk")
+
+
 @pytest.mark.parametrize("dec", ["sp", "rescal+sp"])
 def test_hot_rows_vs_oracle(built_lib, cuda_dev, dec):
     """Collisions at their worst: five entities, every e1 the same entity, one feature in every

@@ -116,3 +116,14 @@ def test_oracle_zero_grad_rows_unchanged():
     O.adagrad_apply(p, acc, g, 0.1)
     assert np.array_equal(p["A"][[0, 1, 3, 4]], before[[0, 1, 3, 4]])
     assert not np.array_equal(p["A"][2], before[2])
+
+
+def test_bf16_round_matches_torch_bfloat16():
+    """The oracle's bf16 operand emulation rounds exactly as a float32 -> bfloat16 conversion
+    (round to nearest, ties to even) -- the v_mfma_f32_16x16x32_bf16 operand rounding."""
+    import torch
+    g = np.random.RandomState(0)
+    x = np.concatenate([g.standard_normal(10000) * 10.0 ** g.randint(-8, 8, 10000),
+                        [0.0, -0.0, 1.0, 1.00390625, 1.01171875, 65504.0, 1e-40]])
+    want = torch.as_tensor(x.astype(np.float32)).to(torch.bfloat16).to(torch.float64).numpy()
+    assert np.array_equal(O.bf16_round(x), want)
