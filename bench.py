@@ -215,6 +215,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--no-label-pass", action="store_true")
+    ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
+                    help="pin a kernel form (include/rae.h; e.g. sp_forward=split); recorded in "
+                         "config.kernel_forms")
     ap.add_argument("--dp-update", default="replicated", choices=["replicated", "partitioned"],
                     help="data-parallel update (N > 1): every rank updates every row, or each "
                          "rank the rows it owns (rows pulled from their owners each step)")
@@ -241,7 +244,8 @@ def main():
                              cfg["s"], 0.0, 0.0, "adagrad", "bench", cfg["dec"], False, True, False,
                              1.0, device=dev, world_size=ws, rank=rk, exchange=exchange,
                              graph_chunk=args.graph_chunk, mfma_bf16=cfg.get("bf16", False),
-                             dp_update=args.dp_update)
+                             dp_update=args.dp_update,
+                             kernel_forms=dict(kv.split("=", 1) for kv in args.kernel_form))
     ind.compile_function()
     eng = ind.engine
     # per-epoch negatives: the reference's RandomState stream, CDF search on the device

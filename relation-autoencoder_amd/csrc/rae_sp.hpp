@@ -569,6 +569,12 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
 }
 
 // ---- the SP example path ---------------------------------------------------------------
+#ifndef RAE_FWD_CFIRST
+#define RAE_FWD_CFIRST 0     // fast path: waves 4-7 issue their decoder-matrix loads before the A rows
+#endif
+#ifndef RAE_FWD_PFLAG
+#define RAE_FWD_PFLAG 0      // fast path: P published by an LDS flag, not a block barrier
+#endif
 template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     const D Dm(a);
@@ -682,7 +688,10 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         const int k = lane + RAE_WAVE * i;
         wbk[i] = (w == 0 && k < m) ? a.Wb[k] : 0.f;
     }
-    if (tid == 0) S.sint[4] = 0;             // arrival counter of the W-row waves
+    if (tid == 0) {
+        S.sint[4] = 0;                       // arrival counter of the W-row waves
+        S.sint[5] = 0;                       // P ready (RAE_FWD_PFLAG)
+    }
     lds_barrier();
     RAE_STAMP(a, 1);
     const int p0 = S.sint[0], nf = S.sint[1];
@@ -733,6 +742,12 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
                 vfma(acc, S.sfval[f], W4[(int64_t)S.sfidx[f] * MV + c]);
             reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
         }
+    } else if (RAE_FWD_CFIRST) {
+        // decoder-matrix slices first: they are needed at C.P, the A rows only after it
+        cc_.load(a, Dm, 0, 0);
+        asm volatile("" ::: "memory");
+        gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
+        if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
     } else {
         gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
         if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
@@ -788,8 +803,21 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         }
         hp = wave_sum(hp);
         if (lane == 0) S.sred[40] = -a.alpha * hp;
+        if (RAE_FWD_PFLAG) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&S.sint[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
-    lds_barrier();
+    if (RAE_FWD_PFLAG) {
+        // P / Z / H ready: an LDS flag instead of a block barrier, so the waves that run the
+        // chain do not wait for waves 4-7 still issuing their bulk loads
+        if (w != 0)
+            while (__hip_atomic_load(&S.sint[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+    } else {
+        lds_barrier();
+    }
     const float H = S.sred[40];
     RAE_STAMP(a, 2);
     sp_project<true>(a, Dm, S, cc_);
