@@ -215,20 +215,28 @@ __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, in
     return (int64_t)nT + nP + NVC + rows;
 }
 
+// LDS of one update workgroup: workgroup tasks' partials (a row: Q vectors per lane, or a tile:
+// 4 floats per lane, per wave) + the Ab partials
+template <bool V4, int Q>
+__host__ __device__ constexpr int update_lds_floats() {
+    return (RAE_NWAVE * Q * RAE_WAVE * (V4 ? 4 : 1) > RAE_NWAVE * RAE_WAVE * 4
+                ? RAE_NWAVE * Q * RAE_WAVE * (V4 ? 4 : 1) : RAE_NWAVE * RAE_WAVE * 4) + RAE_NWAVE;
+}
+
+// wg0 / ngrid: this workgroup's index and the number of workgroups of the update's own grid
+// (the fused bilinear kernel puts the update's workgroups in front of the R-tile ones)
 template <int OPT, bool V4, int Q, bool BIL>
-__device__ __forceinline__ void update_body(const StepArgs& a) {
+__device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngrid, float* lds) {
     typedef typename VecT<V4>::T VT;
-    // workgroup tasks' partials: a row (Q vectors per lane) or a tile (4 floats per lane) per wave
-    constexpr int kRowF = RAE_NWAVE * Q * RAE_WAVE * (V4 ? 4 : 1), kTileF = RAE_NWAVE * RAE_WAVE * 4;
-    __shared__ __attribute__((aligned(16))) float spart_f[kRowF > kTileF ? kRowF : kTileF];
-    __shared__ float sgb[RAE_NWAVE];
-    VT* spart = reinterpret_cast<VT*>(spart_f);
+    constexpr int kF = update_lds_floats<V4, Q>() - RAE_NWAVE;
+    float* sgb = lds + kF;
+    VT* spart = reinterpret_cast<VT*>(lds);
     const int lane = threadIdx.x & 63;
     // wave / workgroup indices as provably uniform values: every task index, row id and
     // record offset derived from them is then scalar (s_load of the segment, SGPR soffsets,
     // scalar branches) instead of VGPR-resident and exec-masked
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wgp = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    const int wgp = __builtin_amdgcn_readfirstlane(wg0);
     const int gw = wgp * RAE_NWAVE + w;
     const int64_t g = step_batch(a);
     const int64_t ex0 = g * (int64_t)a.L;
@@ -241,7 +249,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     // row part first (physical order: very heavy rows, row waves, tiles, cost)
     int wg = wgp;
     if (RAE_ROWS_FIRST) {
-        const int nrow = (int)gridDim.x - nT - nP;
+        const int nrow = ngrid - nT - nP;
         wg = wgp < nrow ? nT + nP + wgp : wgp - nrow;
     }
     const int64_t slot = g % a.index_window;
@@ -302,7 +310,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
     // wave tasks: a wave with several (large global batches: the grid's row part is capped
     // near one resident wave per slot) loads its next task's segment while it works on the
     // current one
-    const int nw = (gridDim.x - nT - nP - a.NVC) * RAE_NWAVE;
+    const int nw = (ngrid - nT - nP - a.NVC) * RAE_NWAVE;
     const int4* tk = reinterpret_cast<const int4*>(a.task) + slot * a.TC;
     int t = (u - a.NVC) * RAE_NWAVE + w;
     int4 seg = tk[t < a.TC ? t : a.TC - 1];
@@ -328,12 +336,37 @@ __device__ __forceinline__ void update_body(const StepArgs& a) {
 #endif
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) RAE_UPD_ATTR void k_update(StepArgs a) {
-    update_body<OPT, V4, Q, false>(a);
+    __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
+    update_body<OPT, V4, Q, false>(a, blockIdx.x, gridDim.x, lds);
 }
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) void k_update_bil(StepArgs a) {
-    update_body<OPT, V4, Q, true>(a);
+    __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
+    update_body<OPT, V4, Q, true>(a, blockIdx.x, gridDim.x, lds);
 }
+// The bilinear decoders' update phase in ONE launch: workgroups [0, gu) run k_update_bil's tasks
+// (Wb tiles, cost, A / W rows: latency-bound chains), the rest k_bil_rows' R tiles (16 rows
+// (i, j) x all m per wave: the HBM-heavy R sweep) -- the two have no data in common, so the
+// row chains run under the R sweep instead of after it.  Dynamic LDS: the R tiles' (DMA'd R and
+// accumulator rows); an update workgroup carves its partials from the same allocation.
+template <int OPT, bool V4, int Q>
+__global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    if (wg < gu) {
+        update_body<OPT, V4, Q, true>(a, wg, gu, reinterpret_cast<float*>(smem));
+        return;
+    }
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = (wg - gu) * RAE_NWAVE + w;
+    if (t >= n_rtiles(a.dec, a.r, a.m)) return;
+    const int slot = n_ctiles(a.dec, a.r, a.m) + t;
+    task_bilinear_rows_lds<OPT>(a, t, slot, threadIdx.x & 63,
+                                reinterpret_cast<float*>(smem) + (size_t)w * (OPT == 0 ? 2 : 1) * 16 * a.m);
+}
+#ifndef RAE_BIL_FUSED_UPD
+#define RAE_BIL_FUSED_UPD 1   // bilinear update phase as one launch (k_bil_update)
+#endif
 
 // Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,
 // reset the scratch, L1/L2 partials of the old W per block (fixed grid -> deterministic).
@@ -958,6 +991,13 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         const int nRt = n_rtiles(a.dec, a.r, a.m);
         const dim3 gr((nRt + RAE_NWAVE - 1) / RAE_NWAVE);
         const size_t lr = bil_rows_lds_bytes(a.m, a.bf16, OPT == 0);
+        constexpr size_t lu = 4 * update_lds_floats<V4, 2>();
+        if (RAE_BIL_FUSED_UPD && lr >= lu) {
+            const dim3 gf(gu.x + gr.x);
+            if (p->q == 1) RAE_LAUNCH(p, (k_bil_update<OPT, V4, 1>), gf, bt, lr, st, a, (int)gu.x);
+            else RAE_LAUNCH(p, (k_bil_update<OPT, V4, 2>), gf, bt, lr, st, a, (int)gu.x);
+            return;
+        }
         if (lr) RAE_LAUNCH(p, (k_bil_rows<OPT, true>), gr, bt, lr, st, a);
         else RAE_LAUNCH(p, (k_bil_rows<OPT, false>), gr, bt, 0, st, a);
         if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);

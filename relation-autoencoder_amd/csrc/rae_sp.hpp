@@ -573,7 +573,7 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
 #define RAE_FWD_CFIRST 0     // fast path: waves 4-7 issue their decoder-matrix loads before the A rows
 #endif
 #ifndef RAE_FWD_PFLAG
-#define RAE_FWD_PFLAG 0      // fast path: P published by an LDS flag, not a block barrier
+#define RAE_FWD_PFLAG 1      // fast path: P published by an LDS flag, not a block barrier
 #endif
 template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
