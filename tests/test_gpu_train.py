@@ -385,8 +385,7 @@ def test_bf16_dp_kernels_agree(built_lib, cuda_dev, dec, shape):
     """The LDS-staged bf16 dP kernel (k_bil_dp2, compiled for the C5 shape and padded for
     others) against the strided bf16 kernel it replaces (bil_dp="strided"): the same bf16 operands,
     only the fp32 summation order differs, so whole runs agree to 5e-4 relative Frobenius
-    distance -- far inside the bf16-vs-float64 tolerance above (which both kernels meet
-    equally: tools/bf16_check.py).  Two batches only: over longer runs the drift between the
+    distance -- far inside the derived bf16-vs-float64 tolerance above.  Two batches only: over longer runs the drift between the
     two orders depends on the trajectory (it grew from 1e-4 to 8e-4 over a five-batch epoch as
     unrelated kernels changed their own rounding)."""
     from rae.data import synthetic_dataset
