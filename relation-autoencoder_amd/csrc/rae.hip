@@ -81,11 +81,10 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
-template <bool BF16, bool DIRECT = false, int RU = -1>
-__global__ __launch_bounds__(RAE_MTT) __attribute__((amdgpu_waves_per_eu(4)))
-void k_bil_mt(StepArgs a, int pass) {
+template <bool BF16, bool DIRECT = false>
+__global__ __launch_bounds__(RAE_MTT) void k_bil_mt(StepArgs a, int pass) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bil_mt<BF16, DIRECT, RU>(a, pass, smem);
+    bil_mt<BF16, DIRECT>(a, pass, smem);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_DBT) void k_bil_dec(StepArgs a) {
@@ -365,9 +364,6 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
     task_bilinear_rows_lds<OPT>(a, t, slot, threadIdx.x & 63,
                                 reinterpret_cast<float*>(smem) + (size_t)w * (OPT == 0 ? 2 : 1) * 16 * a.m);
 }
-#ifndef RAE_RUPD_IN_MT
-#define RAE_RUPD_IN_MT 1      // single-rank bf16 plans: the R update inside the second M-tile pass
-#endif
 #ifndef RAE_BIL_FUSED_UPD
 #define RAE_BIL_FUSED_UPD 1   // bilinear update phase as one launch (k_bil_update)
 #endif
@@ -510,7 +506,6 @@ struct rae_plan {
     size_t smem_dec = 0;
     size_t smem_mt = 0;     // k_bil_mt: one 8 x 16 x m block of R in LDS
     bool mt_direct = false; // fp32 blocks beyond LDS (m > 320): k_bil_mt reads R from L2
-    bool rfused = false;    // the R update runs inside the second M-tile pass (bil_mt_rupdate)
     bool sp_split = false;  // SP forward as enc -> GEMM -> dec -> GEMM -> fin (large shapes)
     size_t smem_spe = 0;    // k_sp_enc
     bool mt_bf16 = false;
@@ -811,10 +806,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
     p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
     p->smem_mt = bil ? bil_mt_lds_bytes(c.relations, p->mt_bf16) : 0;
-    // single rank, bf16 blocks with dP in the second pass, operands written by the forward,
-    // no regulariser: the second pass applies the R update while its block is on chip
-    p->rfused = RAE_RUPD_IN_MT && p->mt_bf16 && mtdp && a.fuse_prep && !a.reg_on &&
-                c.relations % 4 == 0;
+
     if (p->smem_mt > RAE_MT_LDS_MAX) {        // fp32 block too large to stage (m > 320)
         p->mt_direct = true;
         p->smem_mt = 0;
@@ -855,10 +847,6 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
             (void)hipFuncSetAttribute((const void*)k_bil_dp2<8, 8>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<8, 8>());
             (void)hipFuncSetAttribute((const void*)k_bil_mt<true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
-            (void)hipFuncSetAttribute((const void*)k_bil_mt<true, false, 0>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
-            (void)hipFuncSetAttribute((const void*)k_bil_mt<true, false, 1>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
             (void)hipFuncSetAttribute((const void*)k_bil_mt<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
@@ -954,12 +942,7 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 gmt(((a.r + RAE_MTI - 1) / RAE_MTI) * ((a.r + RAE_MTJ - 1) / RAE_MTJ));
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
-        if (p->rfused && pass == 1) {
-            if (a.opt == RAE_OPT_ADAGRAD)
-                RAE_LAUNCH(p, (k_bil_mt<true, false, 0>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
-            else
-                RAE_LAUNCH(p, (k_bil_mt<true, false, 1>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
-        } else if (p->mt_bf16) RAE_LAUNCH(p, (k_bil_mt<true>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
+        if (p->mt_bf16) RAE_LAUNCH(p, (k_bil_mt<true>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
         else if (p->mt_direct) RAE_LAUNCH(p, (k_bil_mt<false, true>), gmt, dim3(RAE_MTT), 0, st, a, pass);
         else RAE_LAUNCH(p, (k_bil_mt<false>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
     }
@@ -1005,11 +988,6 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         if (a.bf16 && !a.fuse_prep) {
             const int gp = 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
             RAE_LAUNCH(p, k_bil_prep, dim3(gp), bt, 0, st, a);
-        }
-        if (p->rfused) {                       // R already updated by the second M-tile pass
-            if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
-            else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
-            return;
         }
         const int nRt = n_rtiles(a.dec, a.r, a.m);
         const dim3 gr((nRt + RAE_NWAVE - 1) / RAE_NWAVE);

@@ -79,10 +79,10 @@ __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
-    load_ids(a, Dm, ex, col, S);
+    load_desc(a, Dm, g, bl, S);
     __syncthreads();
     CCache<V4, DynDims> cc_;
-    encoder_forward<V4, V4, false>(a, Dm, S, 0, 0, cc_);
+    encoder_forward<V4, V4, false>(a, Dm, S, 0, 0, cc_, true);
     const bool hybrid = a.dec == 2;
     if (hybrid) {
         sp_project<V4>(a, Dm, S, cc_);
@@ -165,12 +165,9 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
 #define RAE_MT_STAMP(slot) do { } while (0)
 #endif
 
-template <int OPT> __device__ void bil_mt_rupdate(const StepArgs& a, int i0, int j0, int w, int lane);
-// RU >= 0: the second pass also applies the R update (bil_mt_rupdate<RU>; RU = the optimizer)
-template <bool BF16, bool DIRECT = false, int RU = -1>
+template <bool BF16, bool DIRECT = false>
 __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     static_assert(!(BF16 && DIRECT), "bf16 blocks are always staged (m <= 128)");
-    static_assert(RU < 0 || BF16, "the fused R update needs the bf16 factor copies");
     const int r = a.r, m = a.m, l = a.l;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -415,9 +412,6 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                 }
             }
         }
-    }
-    if constexpr (RU >= 0) {
-        if (pass == 1) bil_mt_rupdate<RU>(a, i0, j0, w, lane);
     }
 }
 
@@ -1133,55 +1127,6 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     const bool ijv = ij < (int64_t)r * r;
     const int ijc = (int)(ijv ? ij : 0);
     bilinear_rows_acc_bf16_ij(a, ijc / r, ijc - (ijc / r) * r, ijv, kg0, nk, acc, lane);
-}
-
-// The R update fused into the second M-tile pass (single rank, bf16, m <= 128, lambda = 0):
-// the workgroup's block holds rows (i0 + w, j0 .. j0 + 15) for wave w -- 16 consecutive rows of
-// the flattened (r^2, m) tensor -- so wave w computes their gradient D[k][row] = sum_b P_bk
-// U_b[i][j] (U from the bf16 factor copies, as k_bil_rows) and applies the optimizer in place.
-// R and its accumulator are read after the block's M-tile and dP work used the staged (old)
-// values; no other workgroup touches the block, and no later kernel of the step reads R.
-template <int OPT>
-__device__ void bil_mt_rupdate(const StepArgs& a, int i0, int j0, int w, int lane) {
-    const int m = a.m, r = a.r;
-    const int li = lane & 15, kk = lane >> 4;
-    const int i = i0 + w, j = j0 + li;
-    const bool ijv = i < r && j < r;
-    if (i >= r) return;                                   // wave-uniform
-    const int nk = (m + 15) / 16;                         // <= RAE_KG (m <= 128)
-    const int64_t row = (int64_t)i * r + (ijv ? j : 0);
-    rae_bf4 acc[RAE_KG];
-#pragma unroll
-    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-    bilinear_rows_acc_bf16_ij<false>(a, i, ijv ? j : 0, ijv, 0, nk, acc, lane);
-    // the parameter reads after the gradient, half the column groups per round trip: the pass
-    // keeps 4 waves per SIMD (<= 128 VGPRs, no spills)
-    constexpr int H = RAE_KG / 2;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        float4 wv[H], av[H];
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-            const int q = h * H + u, k0 = q * 16 + 4 * kk;
-            const bool ok = q < nk && ijv && k0 < m;
-            const int64_t o = ok ? row * m + k0 : 0;
-            wv[u] = ok ? *reinterpret_cast<const float4*>(a.R3 + o) : z4;
-            av[u] = (OPT == 0 && ok) ? *reinterpret_cast<const float4*>(a.aR3 + o) : z4;
-        }
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-            const int q = h * H + u, k0 = q * 16 + 4 * kk;
-            if (!(q < nk && ijv && k0 < m)) continue;
-            float4 wq = wv[u], ac = av[u];
-            float* wp = &wq.x;
-            float* ap = &ac.x;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) wp[e] = opt_update<OPT>(wp[e], &ap[e], acc[q][e], a.lr);
-            *reinterpret_cast<float4*>(a.R3 + row * m + k0) = wq;
-            if (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + row * m + k0) = ac;
-        }
-    }
 }
 
 // One wave: 16 rows ij x all m columns.  The gradient tile comes out transposed (D[k][ij]:

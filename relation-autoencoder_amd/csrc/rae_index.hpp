@@ -219,9 +219,6 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
 //                   light A, light W (the order the update used to derive from the header)
 //   thdr[slot]      (wave tasks, workgroup tasks, 0, 0)
 // W rows are stored as ~row (negative), A rows as row.
-#ifndef RAE_TASK_ORDER
-#define RAE_TASK_ORDER 0     // light rows: 0 A then W, 1 W then A, 2 interleaved
-#endif
 template <int BT>
 __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
     const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];
@@ -240,26 +237,11 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
         if (v < NV) vt[v] = sg;
         else tk[v - NV] = sg;
     }
-    const int LW = hW.y - hW.z;
     for (int t = threadIdx.x; t < T - XV; t += BT) {
         int x = t;
         int4 sg;
         if (x < HA) sg = urA[x];
         else if ((x -= HA) < HW) { sg = urW[x]; sg.x = ~sg.x; }
-        else if (RAE_TASK_ORDER == 1) {          // light W rows (shorter chains) before light A
-            x -= HW;
-            if (x < LW) { sg = urW[a.RW - 1 - x]; sg.x = ~sg.x; }
-            else sg = urA[a.RA - 1 - (x - LW)];
-        } else if (RAE_TASK_ORDER == 2) {        // light A and W rows interleaved
-            x -= HW;
-            const int mn = min(LA, LW);
-            int ia, iw;                          // position among the light A / light W rows
-            if (x < 2 * mn) { ia = (x & 1) ? -1 : x >> 1; iw = (x & 1) ? x >> 1 : -1; }
-            else if (LA > LW) { ia = x - mn; iw = -1; }
-            else { iw = x - mn; ia = -1; }
-            if (ia >= 0) sg = urA[a.RA - 1 - ia];
-            else { sg = urW[a.RW - 1 - iw]; sg.x = ~sg.x; }
-        }
         else if ((x -= HW) < LA) sg = urA[a.RA - 1 - x];
         else { sg = urW[a.RW - 1 - (x - LA)]; sg.x = ~sg.x; }
         tk[XV + t] = sg;

@@ -126,6 +126,24 @@ __device__ __forceinline__ void load_ids(const StepArgs& a, const D& Dm, int64_t
     }
 }
 
+// The example's descriptor (rae_index.hpp build_batch_desc, built with the row index): the NJ
+// entity ids, the CSR start, the feature count and the first dcap feature ids in one coalesced
+// read -- load_ids plus the encoder's feature-id read, one dependent round trip less before the
+// W-row gather.  S.sint[0] = first CSR position, S.sint[2] = feature count.
+template <class D>
+__device__ __forceinline__ void load_desc(const StepArgs& a, const D& Dm, int64_t g, int bl,
+                                          ExampleSmem& S, bool ids = true) {
+    const int NJ = 2 + 2 * Dm.s;                     // ids = false: S has no room for them
+    const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+    for (int t = threadIdx.x; t < a.dstride; t += RAE_FBT) {
+        const int v = dsc[t];
+        if (t == 0) S.sint[2] = v;
+        else if (t == 1) S.sint[0] = v;
+        else if (t < 2 + NJ) { if (ids) S.sids[t - 2] = v; }
+        else if (t - 2 - NJ < a.dcap) S.sfidx[t - 2 - NJ] = v;
+    }
+}
+
 // A-row gather straight into LDS with LDS-DMA (global_load_lds: no VGPR staging; the copy
 // lands while the W rows load).  Row rho -> record j (SP skips e2: j = rho ? rho+1 : 0;
 // bilinear j = rho).  One wave instruction moves 64 lanes x 16 B (V4) or 64 x 4 B; the LDS
@@ -288,11 +306,14 @@ __device__ __forceinline__ void sp_project_back(const StepArgs& a, const D& Dm, 
 // shifted scores z = S - max(S) in S.sZ (log P = z - lse; see softmax_backward).
 template <bool V4, bool V4R, bool LOADC, class D, class Cache>
 __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, ExampleSmem& S,
-                                                int NR, int skip_e2, Cache& cc_) {
+                                                int NR, int skip_e2, Cache& cc_,
+                                                bool desc = false) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
     const int m = Dm.m, mv = m / VW, mp = pad_m(m);
-    const int p0 = S.sint[0], p1 = S.sint[1];
+    // desc: ids and features came with the example's descriptor (load_desc)
+    const int p0 = S.sint[0], p1 = desc ? p0 + S.sint[2] : S.sint[1];
+    const bool have = desc && p1 - p0 <= a.dcap;     // the feature ids are in S.sfidx already
     const int nslot = RAE_FBT / mv > 0 ? RAE_FBT / mv : 1;
     const int slot = threadIdx.x / mv, c = threadIdx.x - slot * mv;
     const VT* Wv = reinterpret_cast<const VT*>(a.W);
@@ -302,7 +323,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     for (int pc = p0; pc < p1; pc += RAE_FBT) {
         const int nf = min(RAE_FBT, p1 - pc);
         if (threadIdx.x < nf) {
-            S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
+            if (!have) S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
             S.sfval[threadIdx.x] = a.values ? a.values[pc + threadIdx.x] : 1.f;
         }
         __syncthreads();
@@ -601,12 +622,12 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
 #else
     constexpr bool kLoadC = CCache<V4, D>::FITS;
 #endif
-    load_ids(a, Dm, ex, col, S);
+    load_desc(a, Dm, g, bl, S);
     __syncthreads();
     RAE_STAMP(a, 1);
     const int NJ = 2 + 2 * s;
     if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
-    encoder_forward<V4, V4, kLoadC>(a, Dm, S, NR, 1, cc_);
+    encoder_forward<V4, V4, kLoadC>(a, Dm, S, NR, 1, cc_, true);
     const float H = S.sred[40];
     RAE_STAMP(a, 2);
     sp_project<V4>(a, Dm, S, cc_);

@@ -26,13 +26,10 @@ __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
     ExampleSmem S = carve_example_smem(smem, 0, m, Dm.r, 0);      // no A rows here
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
-    if (threadIdx.x == 0) {
-        S.sint[0] = a.indptr[ex];
-        S.sint[1] = a.indptr[ex + 1];
-    }
+    load_desc(a, Dm, g, bl, S, false);
     __syncthreads();
     CCache<V4, DynDims> cc_;                                       // unused: no C here
-    encoder_forward<V4, V4, false>(a, Dm, S, 0, 1, cc_);
+    encoder_forward<V4, V4, false>(a, Dm, S, 0, 1, cc_, true);
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     for (int k = threadIdx.x; k < m; k += RAE_FBT) {
         rec[a.lay.oP + k] = S.sP[k];
