@@ -206,6 +206,19 @@ struct RecBuf {
     }
 };
 
+// non-temporal (streaming) row loads / stores, scalar or float4
+typedef float rae_nt4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float ld_nt(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float4 ld_nt(const float4* p) {
+    const rae_nt4 v = __builtin_nontemporal_load(reinterpret_cast<const rae_nt4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float v, float* p) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_nt(float4 v, float4* p) {
+    const rae_nt4 u = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(u, reinterpret_cast<rae_nt4*>(p));
+}
+
 __device__ __forceinline__ void vadd(float& acc, float v) { acc += v; }
 __device__ __forceinline__ void vadd(float4& acc, float4 v) {
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;

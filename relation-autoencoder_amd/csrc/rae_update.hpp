@@ -41,6 +41,10 @@ typedef float rae_f4 __attribute__((ext_vector_type(4)));
 #define RAE_UNRH 8   // record vectors per round on heavy rows (> RAE_UNR1 records; Q = 1)
 #endif
 template <int N> struct IntC { static constexpr int value = N; };
+#ifndef RAE_UPD_NT
+#define RAE_UPD_NT 3 // row parameter traffic: bit 0 non-temporal loads, bit 1 non-temporal stores
+                     // (both: C3 step 19.8 -> 18.5 us, C5 89.3 -> 86.8; profiles/r03_ab.txt)
+#endif
 
 // parameters + accumulators of the tile elements this lane updates (lanes >= 16 of a Wb tile
 // own nothing): loaded up front, in flight with the records
@@ -182,12 +186,16 @@ struct RowVec {
 #pragma unroll
         for (int q = 0; q < Q; ++q) vzero(v[q]);
     }
+    // parameter / accumulator rows stream through once per step: RAE_UPD_NT reads (and
+    // apply_row writes) them non-temporally, so they do not push the exchange records -- read
+    // by many row tasks each -- out of L2
     __device__ __forceinline__ void load(const float* p, int nv, int lane) {
         const VT* pv = reinterpret_cast<const VT*>(p);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int c = lane + RAE_WAVE * q;
-            v[q] = pv[c < nv ? c : 0];
+            if (RAE_UPD_NT & 1) v[q] = ld_nt(pv + (c < nv ? c : 0));
+            else v[q] = pv[c < nv ? c : 0];
         }
     }
 };
@@ -216,8 +224,13 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
         const int c = lane + RAE_WAVE * q;
         if (c < nv) {
             updv<OPT>(pv.v[q], av.v[q], g.v[q], lr);
-            pp[c] = pv.v[q];
-            if (OPT == 0) aa[c] = av.v[q];
+            if (RAE_UPD_NT & 2) {
+                st_nt(pv.v[q], pp + c);
+                if (OPT == 0) st_nt(av.v[q], aa + c);
+            } else {
+                pp[c] = pv.v[q];
+                if (OPT == 0) aa[c] = av.v[q];
+            }
         }
     }
 }
