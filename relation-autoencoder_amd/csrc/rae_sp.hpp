@@ -590,9 +590,6 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
 }
 
 // ---- the SP example path ---------------------------------------------------------------
-#ifndef RAE_FWD_CFIRST
-#define RAE_FWD_CFIRST 0     // fast path: waves 4-7 issue their decoder-matrix loads before the A rows
-#endif
 #ifndef RAE_FWD_PFLAG
 #define RAE_FWD_PFLAG 1      // fast path: P published by an LDS flag, not a block barrier
 #endif
@@ -658,6 +655,10 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
 #endif
 }
+
+// record stores of the fast path
+template <class T>
+__device__ __forceinline__ void rec_st(T* p, T v) { *p = v; }
 
 // ---- the SP example path for compile-time shapes (BASELINE configs) ---------------------
 // Same arithmetic as sp_example, re-timed for a 100-example step where the kernel is a
@@ -763,12 +764,6 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
                 vfma(acc, S.sfval[f], W4[(int64_t)S.sfidx[f] * MV + c]);
             reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
         }
-    } else if (RAE_FWD_CFIRST) {
-        // decoder-matrix slices first: they are needed at C.P, the A rows only after it
-        cc_.load(a, Dm, 0, 0);
-        asm volatile("" ::: "memory");
-        gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
-        if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
     } else {
         gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
         if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
@@ -936,12 +931,12 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
                 vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lane]);
             }
             reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
-            reinterpret_cast<float4*>(rec + (w == 0 ? a.lay.odw1 : a.lay.odw2))[lane] = v;
+            rec_st(reinterpret_cast<float4*>(rec + (w == 0 ? a.lay.odw1 : a.lay.odw2)) + lane, v);
         }
     } else if (w == 2) {                     // V1 = wC1, V2 = wC2
         if (lv) {
-            reinterpret_cast<float4*>(rec + a.lay.oV1)[lane] = wc1;
-            reinterpret_cast<float4*>(rec + a.lay.oV2)[lane] = wc2;
+            rec_st(reinterpret_cast<float4*>(rec + a.lay.oV1) + lane, wc1);
+            rec_st(reinterpret_cast<float4*>(rec + a.lay.oV2) + lane, wc2);
         }
     } else if (w == 3) {                     // G1 = dl wC1 + dr wC2 (A[e1]'s gradient)
         if (lv) {
@@ -950,21 +945,21 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
             gv.y = dl * wc1.y + dr * wc2.y;
             gv.z = dl * wc1.z + dr * wc2.z;
             gv.w = dl * wc1.w + dr * wc2.w;
-            reinterpret_cast<float4*>(rec + a.lay.oG1)[lane] = gv;
+            rec_st(reinterpret_cast<float4*>(rec + a.lay.oG1) + lane, gv);
         }
     } else if (w == 4) {                     // coefficients (c_j, gamma_j) and the loss
         if (tq < s) {
             const int j = 2 + (hi ? s : 0) + tq;
-            rec[a.lay.ocoef + 2 * j] = dg;
-            rec[a.lay.ocoef + 2 * j + 1] = dg;
+            rec_st(rec + a.lay.ocoef + 2 * j, dg);
+            rec_st(rec + a.lay.ocoef + 2 * j + 1, dg);
         }
         const float sls = wave_sum(ls);
         if (lane == 0) {
-            rec[a.lay.ocoef + 0] = 1.f;
-            rec[a.lay.ocoef + 1] = du1;
-            rec[a.lay.ocoef + 2] = 0.f;
-            rec[a.lay.ocoef + 3] = du2;
-            rec[a.lay.oloss] = -spu1 - spu2 + 2.f * H + sls;
+            rec_st(rec + a.lay.ocoef + 0, 1.f);
+            rec_st(rec + a.lay.ocoef + 1, du1);
+            rec_st(rec + a.lay.ocoef + 2, 0.f);
+            rec_st(rec + a.lay.ocoef + 3, du2);
+            rec_st(rec + a.lay.oloss, -spu1 - spu2 + 2.f * H + sls);
         }
     }
     lds_barrier();
@@ -1067,8 +1062,8 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         for (int i = 0; i < NI; ++i) {
             const int k = lane + RAE_WAVE * i;
             if (k < m) {
-                rec[a.lay.oP + k] = pk[i];
-                rec[a.lay.odS + k] = pk[i] * ((dp[i] - sd) + ce * (zk[i] - sz));
+                rec_st(rec + a.lay.oP + k, pk[i]);
+                rec_st(rec + a.lay.odS + k, pk[i] * ((dp[i] - sd) + ce * (zk[i] - sz)));
             }
         }
     }
