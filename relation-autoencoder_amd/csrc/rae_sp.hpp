@@ -593,6 +593,9 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
 #ifndef RAE_FWD_PFLAG
 #define RAE_FWD_PFLAG 1      // fast path: P published by an LDS flag, not a block barrier
 #endif
+#ifndef RAE_FWD_CWAIT
+#define RAE_FWD_CWAIT 1      // fast path: C loads last on every wave, C.P in load order
+#endif
 template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     const D Dm(a);
@@ -656,6 +659,21 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
 #endif
 }
 
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4; M0 = the wave-uniform LDS row base) as
+// inline asm: the compiler's wait-count pass treats every LDS access behind an LDS-DMA it can
+// see as a possible alias and puts a vmcnt(0) -- every outstanding load -- in front of it, which
+// in the fast path serialised the W-row partial sums, the P hand-off and C.P behind the whole
+// 160 KB of decoder-matrix loads.  Issued before those loads, an LDS-DMA the pass cannot see
+// only ever makes its counted waits wait for more (vmcnt retires in issue order); the rows are
+// read after dma_visible_barrier (vmcnt(0) + barrier).
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+__device__ __forceinline__ void dma_row16(const float* gsrc, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(gsrc), "s"(lds) : "memory", "m0");
+}
+
 // record stores of the fast path
 template <class T>
 __device__ __forceinline__ void rec_st(T* p, T v) { *p = v; }
@@ -680,6 +698,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
+    float* const arows = S.srows;
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
@@ -717,7 +736,15 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     lds_barrier();
     RAE_STAMP(a, 1);
     const int p0 = S.sint[0], nf = S.sint[1];
+#if RAE_FWD_CWAIT
+    // rows with more features than the W-row registers hold (NSL*KF = 30 at C3; the synthetic
+    // C3 rows have 9..39, P(nf > 30) ~ 1e-6) take the general path: then the decoder-matrix
+    // loads are the LAST vector-memory ops of every wave, so C.P waits for each C load by a
+    // counted vmcnt and runs while the rest of C lands
+    if (nf > a.dcap || nf > NSL * KF) {
+#else
     if (nf > a.dcap) {                       // longer than the descriptor holds: general path
+#endif
         lds_barrier();
         sp_example<true, D>(a, g, bl, smem);
         return;
@@ -752,7 +779,41 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     // FMAs sees only the 28 decoder-matrix loads behind them (not the DMA loop).
     float abv = 0.f;
     CCache<true, D> cc_;
+#if RAE_FWD_CWAIT
+    // the decoder-matrix loads are issued by common code after the role branch: issued in one
+    // place, their registers need no copies where the role paths merge (copies of a loaded
+    // register wait for it, which had put a vmcnt(0) -- all of C -- in front of C.P)
+    if (w >= 4) {
+        // A rows by LDS-DMA, one row per wave instruction (r / 4 = 50 lanes x 16 B), rows
+        // w-4, w, w+4, ...: a fixed unrolled count (no loop, so the vmcnt bookkeeping of the
+        // C loads behind it stays exact)
+        static_assert(r / 4 <= RAE_WAVE, "one DMA instruction per A row");
+        constexpr int RPW4 = (NR + 3) / 4;
+        const int ln = lane < r / 4 ? lane : 0;
+#pragma unroll
+        for (int k = 0; k < RPW4; ++k) {
+            const int rho = (w - 4) + 4 * k;
+            if (rho < NR && lane < r / 4) {
+                const int j = rho == 0 ? 0 : rho + 1;            // SP: e2's row is not read
+                const float* src = a.A + (int64_t)S.sids[j] * r + (int64_t)ln * 4;
+                dma_row16(src, lds_addr(arows + rho * r4));
+            }
+        }
+        if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
+    }
+    asm volatile("" ::: "memory");
+    cc_.load(a, Dm, 0, 0);
     if (w < 4) {
+        float4 acc;
+        vzero(acc);
+#pragma unroll
+        for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
+        if (slot < NSL) reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
+    }
+    if (false) {
+#else
+    if (w < 4) {
+#endif
         asm volatile("" ::: "memory");
         cc_.load(a, Dm, 0, 0);
         float4 acc;
@@ -760,11 +821,13 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
 #pragma unroll
         for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
         if (slot < NSL) {
+#if !RAE_FWD_CWAIT
             for (int f = slot + NSL * KF; f < nf; f += NSL)      // rows with > NSL*KF features
                 vfma(acc, S.sfval[f], W4[(int64_t)S.sfidx[f] * MV + c]);
+#endif
             reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
         }
-    } else {
+    } else if (!RAE_FWD_CWAIT) {
         gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
         if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
         asm volatile("" ::: "memory");
@@ -836,7 +899,43 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     }
     const float H = S.sred[40];
     RAE_STAMP(a, 2);
+#if RAE_FWD_CWAIT
+    {
+        // wC1 = C1.P, wC2 = C2.P: the 2*RA partial dots in C's load order (each waits for its
+        // own loads only), then the 2*RA group reductions as independent interleaved DPP
+        // chains, then one masked store block
+        typedef CCache<true, D> CC_;
+        static_assert(CC_::FITS && CC_::CC == 2, "fast path keeps C1/C2 in registers");
+        const int gid = tid >> 4, q = tid & 15;
+        const float4* Pv = reinterpret_cast<const float4*>(S.sP);
+        const float4 pa = Pv[q], pb = Pv[q + 16];              // zero beyond m (padded)
+        float s1[CC_::RA], s2[CC_::RA];
+#pragma unroll
+        for (int ra = 0; ra < CC_::RA; ++ra) {
+            s1[ra] = vdot(cc_.c1[ra][0], pa);
+            s2[ra] = vdot(cc_.c2[ra][0], pa);
+            s1[ra] += vdot(cc_.c1[ra][1], pb);
+            s2[ra] += vdot(cc_.c2[ra][1], pb);
+        }
+#pragma unroll
+        for (int ra = 0; ra < CC_::RA; ++ra) {
+            s1[ra] = group16_sum(s1[ra]);
+            s2[ra] = group16_sum(s2[ra]);
+        }
+        if (q == 0) {
+#pragma unroll
+            for (int ra = 0; ra < CC_::RA; ++ra) {
+                const int i = gid + RAE_NG * ra;
+                if (i < r) {
+                    S.swC1[i] = s1[ra];
+                    S.swC2[i] = s2[ra];
+                }
+            }
+        }
+    }
+#else
     sp_project<true>(a, Dm, S, cc_);
+#endif
     if (w >= 4 && tid - 256 < NJ) S.sAbv[tid - 256] = abv;
     dma_visible_barrier();                   // A rows (LDS-DMA) and Ab landed
     RAE_STAMP(a, 3);
@@ -847,7 +946,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     static_assert(RV <= RAE_WAVE, "one float4 column per lane");
     const bool lv = lane < RV;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* Rv = reinterpret_cast<const float4*>(S.srows);
+    const float4* Rv = reinterpret_cast<const float4*>(arows);
     // branch-free: every lane reads a valid LDS float4 (lanes past the row re-read column 0)
     // and is zeroed through wc, so all the wave's LDS reads issue back to back
     const int lc = lv ? lane : 0;
