@@ -168,6 +168,10 @@ int64_t rae_index_window(rae_plan* plan);
  * plan) so a captured sequence of steps can be replayed for successive batches.        */
 int rae_set_cursor(rae_plan* plan, int64_t batch, rae_stream_t stream);
 int rae_advance_cursor(rae_plan* plan, int64_t count, rae_stream_t stream);
+/* Number of rae_set_cursor / rae_advance_cursor calls made on this plan so far (host count;
+ * a captured graph's replays make no calls).  A driver that caches where the cursor points
+ * compares it with the count it saw last, so a move made by anyone else is never missed.  */
+int64_t rae_cursor_moves(const rae_plan* plan);
 /* K1: per-example encoder + decoder forward/backward of this rank's l examples.  Writes the
  * exchange records.  The batch's row index must have been built (rae_build_index).      */
 int rae_step_forward(rae_plan* plan, int64_t step_offset, rae_stream_t stream);

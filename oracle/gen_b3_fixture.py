@@ -19,6 +19,7 @@ Usage:  python oracle/gen_b3_fixture.py [out.json]
 """
 from __future__ import annotations
 
+import hashlib
 import importlib.util
 import json
 import os
@@ -53,6 +54,12 @@ def load_reference_evaluator():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def source_sha256():
+    """sha256 of the evaluator file the fixture was produced from (recorded in the fixture)."""
+    with open(os.path.join(REF, "evaluation", "OieEvaluation.py"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
 
 
 def _cases():
@@ -106,7 +113,7 @@ def main(out=OUT):
         print(f"{c['name']}: f1 {f1:.12f} pre {pre:.12f} rec {rec:.12f}")
     with open(out, "w") as fh:
         json.dump({"source": "evaluation/OieEvaluation.py executed by oracle/gen_b3_fixture.py",
-                   "cases": res}, fh, indent=0, sort_keys=True)
+                   "source_sha256": source_sha256(), "cases": res}, fh, indent=0, sort_keys=True)
 
 
 if __name__ == "__main__":

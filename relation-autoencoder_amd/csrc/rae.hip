@@ -498,6 +498,7 @@ struct rae_plan {
     rae_buffers buf;
     StepArgs args;
     int64_t* d_cursor = nullptr;
+    int64_t cursor_moves = 0;  // host count of rae_set_cursor / rae_advance_cursor calls
     int64_t* d_zero = nullptr;
     int* d_err = nullptr;
     char* ws = nullptr;
@@ -899,15 +900,18 @@ extern "C" int rae_set_negatives(rae_plan* p, const int32_t* n1, const int32_t* 
 extern "C" int rae_set_cursor(rae_plan* p, int64_t batch, rae_stream_t stream) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     hipLaunchKernelGGL(k_set_cursor, dim3(1), dim3(64), 0, (hipStream_t)stream, p->d_cursor, batch);
+    ++p->cursor_moves;
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }
 extern "C" int rae_advance_cursor(rae_plan* p, int64_t count, rae_stream_t stream) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     hipLaunchKernelGGL(k_add_cursor, dim3(1), dim3(64), 0, (hipStream_t)stream, p->d_cursor, count);
+    ++p->cursor_moves;
     HIPCHK(hipGetLastError());
     return RAE_OK;
 }
+extern "C" int64_t rae_cursor_moves(const rae_plan* p) { return p ? p->cursor_moves : -1; }
 
 static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 gr(p->grid_fwd), bt(RAE_FBT);

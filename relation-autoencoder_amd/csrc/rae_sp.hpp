@@ -602,8 +602,6 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     const int m = Dm.m, r = Dm.r, s = Dm.s, NR = 1 + 2 * s;
     const int r4 = align4(r), mp = pad_m(m);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int VW = V4 ? 4 : 1;
-    typedef typename VecT<V4>::T VT;
     ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;

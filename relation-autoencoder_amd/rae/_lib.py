@@ -68,8 +68,8 @@ RAE_NEG_PER_EPOCH = 1
 EXPORTS = (
     "rae_plan_create", "rae_plan_destroy", "rae_last_error", "rae_version", "rae_build_id",
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
-    "rae_set_cursor", "rae_advance_cursor", "rae_step_forward", "rae_step_update",
-    "rae_step_forward_at", "rae_step_update_at",
+    "rae_set_cursor", "rae_advance_cursor", "rae_cursor_moves", "rae_step_forward",
+    "rae_step_update", "rae_step_forward_at", "rae_step_update_at",
     "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
@@ -161,6 +161,8 @@ def load(path: str | None = None):
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]
     lib.rae_advance_cursor.argtypes = [_P, C.c_int64, _P]
+    lib.rae_cursor_moves.argtypes = [_P]
+    lib.rae_cursor_moves.restype = C.c_int64
     lib.rae_step_forward.argtypes = [_P, C.c_int64, _P]
     lib.rae_step_update.argtypes = [_P, C.c_int64, _P]
     lib.rae_step_forward_at.argtypes = [_P, C.c_int64, _P]

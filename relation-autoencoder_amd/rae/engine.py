@@ -176,10 +176,12 @@ class TrainEngine:
         self.graph_absolute = bool(graph_absolute)
         # batch the device cursor holds after this engine's last cursor-driven run (None:
         # unknown); run() skips its rae_set_cursor launch when the cursor already points at
-        # the requested batch (consecutive runs of an epoch).  Every cursor move goes through
-        # this engine (set_cursor / run); a caller driving the plan directly calls
-        # cursor_moved() afterwards.
+        # the requested batch (consecutive runs of an epoch).  The plan counts every cursor
+        # move made through the ABI (rae_cursor_moves): a move by anyone but this engine --
+        # a direct rae_set_cursor / rae_advance_cursor on its plan -- changes the count, and
+        # run() then sets the cursor again (cursor_moved() forces the same).
         self._cursor_at = None
+        self._moves_seen = self._moves()
 
     # ------------------------------------------------------------------ partitioned update
     def _dp_caps_check(self):
@@ -250,10 +252,14 @@ class TrainEngine:
                 "bil_prep": ("kernel" if out.bil_prep == 1 else "fused") if bf16 else None,
                 "dp_update": name["dp_update"][out.dp_update]}
 
+    def _moves(self):
+        return int(self.lib.rae_cursor_moves(self.plan))
+
     def set_cursor(self, batch: int):
         """Point the device cursor at global batch `batch` (stream-ordered)."""
         _lib.check(self.lib.rae_set_cursor(self.plan, int(batch), self._stream()), "rae_set_cursor")
         self._cursor_at = int(batch)
+        self._moves_seen = self._moves()
 
     def cursor_moved(self):
         """Tell the engine the device cursor was driven outside run() (direct rae_set_cursor /
@@ -370,6 +376,8 @@ class TrainEngine:
         key = (count if advance else ("last", count)) if first is None else (int(first), count)
         g = self._graphs.get(key)
         if g is None:
+            # the capture calls rae_advance_cursor once (recorded, not run): not a real move
+            in_sync = self._moves_seen == self._moves()
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -378,6 +386,8 @@ class TrainEngine:
             torch.cuda.current_stream(self.device).wait_stream(s)
             _upload_graph(g, s)
             self._graphs[key] = g
+            if in_sync:
+                self._moves_seen = self._moves()
         return g
 
     def _chunks(self, first_batch: int, count: int):
@@ -475,7 +485,7 @@ class TrainEngine:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
                 continue
-            if self._cursor_at != b:
+            if self._cursor_at != b or self._moves_seen != self._moves():
                 self.set_cursor(b)
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
@@ -486,6 +496,7 @@ class TrainEngine:
                 for cnt, adv in reps:
                     self._graph(cnt, advance=adv).replay()
                 self._cursor_at = b + n - (0 if reps[-1][1] else reps[-1][0])
+            self._moves_seen = self._moves()
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):

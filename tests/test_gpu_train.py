@@ -366,8 +366,8 @@ def test_consecutive_runs_skip_cursor_reset(built_lib, cuda_dev):
                 import ctypes as C
                 import torch
                 st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+                # a direct ABI move, no cursor_moved(): the plan's move count tells the engine
                 assert eng.lib.rae_set_cursor(eng.plan, 17, st) == 0
-                eng.cursor_moved()
             eng.run(5, nb - 5)
         import torch
         torch.cuda.synchronize()
