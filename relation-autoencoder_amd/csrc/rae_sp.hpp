@@ -596,6 +596,9 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
 #ifndef RAE_FWD_CWAIT
 #define RAE_FWD_CWAIT 1      // fast path: C loads last on every wave, C.P in load order
 #endif
+#ifndef RAE_FWD_CEARLY47
+#define RAE_FWD_CEARLY47 0   // fast path: waves 4-7 issue their C share at kernel start
+#endif
 template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     const D Dm(a);
@@ -705,6 +708,12 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 #endif
+    CCache<true, D> cc_;
+#if RAE_FWD_CWAIT && RAE_FWD_CEARLY47
+    // waves 4-7 have no load on the chain: their half of C goes out at once (the other half
+    // follows the W rows of waves 0-3), so C's ingest starts ~1 us earlier
+    if (w >= 4) cc_.load(a, Dm, 0, 0);
+#endif
     // the example's descriptor (rae_index.hpp build_batch_desc): feature count, CSR start,
     // entity ids and feature ids in one coalesced read
     {
@@ -776,7 +785,6 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     // Each role is one uniform branch, so the compiler's vmcnt bookkeeping for the W-row
     // FMAs sees only the 28 decoder-matrix loads behind them (not the DMA loop).
     float abv = 0.f;
-    CCache<true, D> cc_;
 #if RAE_FWD_CWAIT
     // the decoder-matrix loads are issued by common code after the role branch: issued in one
     // place, their registers need no copies where the role paths merge (copies of a loaded
@@ -800,7 +808,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         if (tid - 256 < NJ) abv = a.Ab[S.sids[tid - 256]];
     }
     asm volatile("" ::: "memory");
-    cc_.load(a, Dm, 0, 0);
+    if (!RAE_FWD_CEARLY47 || w < 4) cc_.load(a, Dm, 0, 0);
     if (w < 4) {
         float4 acc;
         vzero(acc);
