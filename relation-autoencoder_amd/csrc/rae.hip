@@ -81,6 +81,11 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode<V4>(a, step_batch(a), blockIdx.x, smem);
 }
+template <class D>
+__global__ __launch_bounds__(RAE_FBT) void k_bil_enc_fast(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bil_encode_fast<D>(a, step_batch(a), blockIdx.x, smem);
+}
 template <bool BF16, bool DIRECT = false>
 __global__ __launch_bounds__(RAE_MTT) void k_bil_mt(StepArgs a, int pass) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -832,6 +837,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                              (const void*)k_forward<true, DynDims>,
                              (const void*)k_forward<false, DynDims>,
                              (const void*)k_bil_enc<true>, (const void*)k_bil_enc<false>,
+                             (const void*)k_bil_enc_fast<DimsC3>,
                              (const void*)k_sp_dec<true>, (const void*)k_sp_dec<false>};
         for (const void* f : fns)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -942,7 +948,10 @@ static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st);
 template <bool V4>
 static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 ge(p->grid_fwd);
-    RAE_LAUNCH(p, (k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
+    if (V4 && a.dec == RAE_DEC_RESCAL && a.m == 100 && a.r == 200 && a.s == 20)     // C5 shape
+        RAE_LAUNCH(p, (k_bil_enc_fast<DimsC3>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
+    else
+        RAE_LAUNCH(p, (k_bil_enc<V4>), ge, dim3(RAE_FBT), p->smem_fwd, st, a);
     const dim3 gmt(((a.r + RAE_MTI - 1) / RAE_MTI) * ((a.r + RAE_MTJ - 1) / RAE_MTJ));
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);

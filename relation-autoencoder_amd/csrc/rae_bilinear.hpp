@@ -110,6 +110,104 @@ __device__ void bil_encode(const StepArgs& a, int64_t g, int bl, char* smem) {
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];     // H until k_bil_dec
 }
 
+// k_bil_enc for compile-time shapes (C5: K = 100, r = 200), RESCAL: the SP fast path's encoder
+// -- the example's descriptor in one read, the W rows on waves 0-3, the softmax in wave 0 behind
+// an LDS arrival counter (no block barrier) -- while waves 4-5 copy A[e1] / A[e2] into the
+// record (and their bf16 factor copies) and waves 6-7 zero V1 / V2.  Rows with more features
+// than the W-row registers hold, and the hybrid (its C.P), take bil_encode.
+template <class D>
+__device__ void bil_encode_fast(const StepArgs& a, int64_t g, int bl, char* smem) {
+    static_assert(D::fixed && D::m % 4 == 0 && D::r % 4 == 0 && D::r / 4 <= RAE_WAVE, "fast encoder");
+    constexpr int m = D::m, r = D::r, s = D::s, NJ = 2 + 2 * s;
+    constexpr int MV = m / 4, NSL = 256 / MV, KF = 3, RV = r / 4;
+    constexpr int mp = ((m + 255) / 256) * 256, NI = mp / RAE_WAVE;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    ExampleSmem S = carve_example_smem(smem, a.dec, m, r, s);
+    const int bg = a.rank * a.l + bl;
+    {
+        const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+        if (tid < a.dstride) {
+            const int v = dsc[tid];
+            if (tid == 0) S.sint[1] = v;                          // nf
+            else if (tid == 1) S.sint[0] = v;                     // p0
+            else if (tid < 2 + NJ) S.sids[tid - 2] = v;
+            else if (tid - 2 - NJ < 256) S.sfidx[tid - 2 - NJ] = v;
+        }
+    }
+    float wbk[NI];                           // wave 0: the bias entries it reduces
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        wbk[i] = (w == 0 && k < m) ? a.Wb[k] : 0.f;
+    }
+    if (tid == 0) S.sint[4] = 0;             // arrival counter of the W-row waves
+    lds_barrier();
+    const int p0 = S.sint[0], nf = S.sint[1];
+    if (nf > a.dcap || nf > NSL * KF) {
+        lds_barrier();
+        bil_encode<true>(a, g, bl, smem);
+        return;
+    }
+    if (a.values) {
+        if (w < 4 && tid < nf) S.sfval[tid] = a.values[p0 + tid];
+        lds_barrier();
+    }
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (w < 4) {
+        // W rows: slot = feature lane group, c = float4 column; the partial sums into LDS
+        const float4* W4 = reinterpret_cast<const float4*>(a.W);
+        const int slot = tid / MV, c = tid - slot * MV;
+        float4 wv[KF];
+        float fv[KF];
+#pragma unroll
+        for (int k = 0; k < KF; ++k) {
+            const int f = slot + NSL * k;
+            const bool ok = slot < NSL && f < nf;
+            const int fi = S.sfidx[f < 256 ? f : 255];
+            wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
+            fv[k] = ok ? (a.values ? S.sfval[f < 256 ? f : 255] : 1.f) : 0.f;
+        }
+        float4 acc = z4;
+#pragma unroll
+        for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
+        if (slot < NSL) reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&S.sint[4], 1);
+    } else if (w < 6) {
+        // copies of A[e1] (wave 4) / A[e2] (wave 5), taken before the update changes A
+        if (lane < RV) {
+            const float4 v = reinterpret_cast<const float4*>(a.A + (int64_t)S.sids[w - 4] * r)[lane];
+            reinterpret_cast<float4*>(rec + (w == 4 ? a.lay.oA1 : a.lay.oA2))[lane] = v;
+            if (a.fuse_prep) {
+                put_fac(a, w - 3, 4 * lane + 0, bg, v.x);
+                put_fac(a, w - 3, 4 * lane + 1, bg, v.y);
+                put_fac(a, w - 3, 4 * lane + 2, bg, v.z);
+                put_fac(a, w - 3, 4 * lane + 3, bg, v.w);
+            }
+        }
+    } else if (lane < RV) {                  // V1 / V2 = 0 (no SP part)
+        reinterpret_cast<float4*>(rec + (w == 6 ? a.lay.oV1 : a.lay.oV2))[lane] = z4;
+    }
+    if (w == 0) {
+        while (__hip_atomic_load(&S.sint[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
+            __builtin_amdgcn_s_sleep(1);
+        float pz[NI], pp[NI];
+        fast_softmax<m, NSL, NI>(a, S, wbk, lane, pz, pp);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int k = lane + RAE_WAVE * i;
+            if (k < m) {
+                rec[a.lay.oP + k] = pp[i];
+                rec[a.lay.oZ + k] = pz[i];
+                if (a.fuse_prep) prep_p_fragment(a, bg, k, pp[i]);
+            }
+        }
+        if (lane == 0) rec[a.lay.oloss] = S.sred[40];       // H until k_bil_dec
+    }
+}
+
 // ---- bf16 fragments -----------------------------------------------------------------------
 // v_mfma_f32_16x16x32_bf16: lane l holds A[l&15][8(l>>4) + e] and B[8(l>>4) + e][l&15],
 // e = 0..7; fp32 values are rounded to bf16 (nearest even) as they enter the fragment,

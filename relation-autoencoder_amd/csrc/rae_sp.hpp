@@ -679,6 +679,53 @@ __device__ __forceinline__ void dma_row16(const float* gsrc, uint32_t lds) {
 template <class T>
 __device__ __forceinline__ void rec_st(T* p, T v) { *p = v; }
 
+// Wave 0 of a fast path, once the W-row partial sums of the NSL feature slots are in S.spart:
+// S = X.W + Wb, softmax and entropy -- z = S - max S and P into S.sZ / S.sP (and pz / pp: the
+// lane's entries k = lane + 64 i), H (alpha-scaled) into S.sred[40].
+template <int m, int NSL, int NI>
+__device__ __forceinline__ void fast_softmax(const StepArgs& a, ExampleSmem& S, const float (&wbk)[NI],
+                                             int lane, float (&pz)[NI], float (&pp)[NI]) {
+    float sv[NI];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        float v = 0.f;
+        if (k < m) {
+#pragma unroll
+            for (int sl = 0; sl < NSL; ++sl) v += S.spart[sl * m + k];
+            v += wbk[i];
+            mx = fmaxf(mx, v);
+        }
+        sv[i] = v;
+    }
+    mx = wave_max(mx);
+    float ev[NI];
+    float se = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        ev[i] = k < m ? __expf(sv[i] - mx) : 0.f;
+        se += ev[i];
+    }
+    se = wave_sum(se);
+    const float inv = 1.f / se, lse = __logf(se);
+    float hp = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        const float z = k < m ? sv[i] - mx : 0.f;
+        const float p = ev[i] * inv;
+        S.sZ[k] = z;
+        S.sP[k] = p;
+        pz[i] = z;
+        pp[i] = p;
+        hp += p * (z - lse);
+    }
+    hp = wave_sum(hp);
+    if (lane == 0) S.sred[40] = -a.alpha * hp;
+}
+
 // ---- the SP example path for compile-time shapes (BASELINE configs) ---------------------
 // Same arithmetic as sp_example, re-timed for a 100-example step where the kernel is a
 // dependent chain: waves 0-3 run the critical chain (ids -> feature ids -> W rows -> S ->
@@ -851,43 +898,8 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         while (__hip_atomic_load(&S.sint[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
             __builtin_amdgcn_s_sleep(1);
         RAE_STAMP(a, 13);
-        float sv[NI];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int k = lane + RAE_WAVE * i;
-            float v = 0.f;
-            if (k < m) {
-#pragma unroll
-                for (int sl = 0; sl < NSL; ++sl) v += S.spart[sl * m + k];
-                v += wbk[i];
-                mx = fmaxf(mx, v);
-            }
-            sv[i] = v;
-        }
-        mx = wave_max(mx);
-        float ev[NI];
-        float se = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int k = lane + RAE_WAVE * i;
-            ev[i] = k < m ? __expf(sv[i] - mx) : 0.f;
-            se += ev[i];
-        }
-        se = wave_sum(se);
-        const float inv = 1.f / se, lse = __logf(se);
-        float hp = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int k = lane + RAE_WAVE * i;
-            const float z = k < m ? sv[i] - mx : 0.f;
-            const float p = ev[i] * inv;
-            S.sZ[k] = z;
-            S.sP[k] = p;
-            hp += p * (z - lse);
-        }
-        hp = wave_sum(hp);
-        if (lane == 0) S.sred[40] = -a.alpha * hp;
+        float pz[NI], pp[NI];
+        fast_softmax<m, NSL, NI>(a, S, wbk, lane, pz, pp);
         if (RAE_FWD_PFLAG) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_store(&S.sint[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

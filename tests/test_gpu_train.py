@@ -473,7 +473,7 @@ def test_c1_data_sample_vs_oracle(built_lib, cuda_dev, dec, m, hp):
         assert f[0] == f[1]
 
 
-def _edge_dataset(seed=11):
+def _edge_dataset(seed=11, mid_rows=False):
     """Ragged inputs the reference accepts: examples with no features (every feature of the
     example thresholded away, OiePreprocessor.py:200-208 -> an empty CSR row), examples longer
     than the fast path's descriptor (general path), e1 == e2, negatives equal to the positive
@@ -484,6 +484,8 @@ def _edge_dataset(seed=11):
     lens = g.randint(1, 20, size=N)
     lens[::17] = 0                                   # empty rows
     lens[5::97] = 300                                # longer than the descriptor capacity
+    if mid_rows:                                     # around the fast paths' W-row registers (30)
+        lens[3::11] = g.randint(25, 64, size=len(lens[3::11]))
     rows = np.repeat(np.arange(N), lens)
     cols = np.concatenate([g.choice(d, size=k, replace=False) for k in lens])
     X = sp.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(N, d))
@@ -522,6 +524,26 @@ def test_ragged_inputs_vs_oracle(built_lib, cuda_dev, dec):
     # empty rows score Wb alone: one shared label
     empty = np.flatnonzero(np.diff(X.indptr)[:len(want)] == 0)
     assert len(set(lab[empty].tolist())) == 1
+
+
+@pytest.mark.parametrize("dec", ["sp", "rescal"])
+def test_fast_paths_ragged_vs_oracle(built_lib, cuda_dev, dec):
+    """The compile-time-shape kernels (C3's SP forward, C5's RESCAL encoder: K=100, r=200, s=20)
+    on ragged rows: empty rows, rows around the 30 features their W-row registers hold and rows
+    longer than the descriptor -- the longer rows take the runtime-shape path inside the same
+    launch."""
+    from rae.inducer import ReconstructInducer
+    data = _edge_dataset(mid_rows=True)
+    nf = np.diff(data.split["train"].xFeats.indptr)
+    assert nf.min() == 0 and ((nf > 30) & (nf < 64)).any() and nf.max() == 300
+    m, r, s, l, ep = 100, 200, 20, 100, 1
+    ind = ReconstructInducer(data, {"train": {}}, np.random.RandomState(2), ep, 0.1, l, r, m, s,
+                             0.0, 0.0, "adagrad", "edge", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2)
+    ind.learn(verbose=False)
+    tr, costs = _oracle_trajectory(dec, data, 2, m, r, s, l, ep, lr=0.1, alpha=1.0)
+    np.testing.assert_allclose(np.array(ind.epoch_costs), costs, rtol=COST_RTOL, atol=COST_RTOL)
+    _assert_params_close(_params(ind), tr.params, "ragged-fast")
 
 
 @pytest.mark.parametrize("m", [12, 100, 300, 7])      # 16 / 32 / 64 lanes per row; scalar path
