@@ -234,7 +234,9 @@ __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
 // Partials per j-block / i-block are summed in block order by the consumer (k_bil_dec for
 // pass 1: v = M a2, w = M^T a1; k_bil_fin for pass 2: M y, M^T x) -- deterministic.  R is read
 // once per pass; (r/8)(r/16) workgroups (325 at r = 200: every block's staging in one round).
-#define RAE_MTI 8         // rows i per block
+#ifndef RAE_MTI
+#define RAE_MTI 8         // rows i per block (a multiple of 4)
+#endif
 #define RAE_MTJ 16        // columns j per block (one MFMA tile of rows)
 #define RAE_MTT RAE_FBT   // threads per k_bil_mt workgroup (8 waves)
 #define RAE_MTW (RAE_MTT / RAE_WAVE)
@@ -242,6 +244,8 @@ __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
 // bf16: the block image [(i,j)][KP + 8] and, for the dP contraction of the second pass, its
 // transpose [k][pairs + 8] (every B fragment one ds_read_b128)
 #define RAE_MT_TP (RAE_MTI * RAE_MTJ + 8)
+#define RAE_MT_NKS (RAE_MTI * RAE_MTJ / 32)   // K steps of the dP contraction (32 pairs each)
+static_assert(RAE_MTI % 4 == 0 && RAE_MTJ == 16, "M-tile blocks: 4k rows i x 16 columns j");
 __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
     const int KP = (m + 31) / 32 * 32;
     return bf16 ? (size_t)RAE_MTI * RAE_MTJ * (KP + 8) * 2 + (size_t)KP * RAE_MT_TP * 2
@@ -339,6 +343,36 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     const int ov = pass == 0 ? a.lay.oA2 : a.lay.oY;      // cv: contracted over j
     const int ow = pass == 0 ? a.lay.oA1 : a.lay.oX;      // cw: contracted over i
     const int nbt = (l + 15) / 16;
+    // dP operands of the second pass (bf16), for lane (li, g) of an example tile: a2 / y at
+    // j0 + 8 (g&1) .. +7 and x / a1 at rows i0 + 2 ks + g/2, ks < RAE_MT_NKS (unconditional loads of
+    // clamped addresses, then selects: a conditional load becomes a flat load through a zeroed
+    // scratch slot)
+    const bool dpass = BF16 && pass == 1 && a.mtP != nullptr;
+    struct DpOps { float a2v[8], yv[8], xq[RAE_MT_NKS], cq[RAE_MT_NKS]; };
+    auto load_dp = [&](DpOps& o, const float* erb, bool bv) {
+        const int jh = j0 + 8 * (g & 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = jh + 4 * h;                // r4 padding of the record is zero
+            const bool ok = bv && j < r;
+            const int jc = j < r ? j : 0;
+            const float4 va = *reinterpret_cast<const float4*>(erb + a.lay.oA2 + jc);
+            const float4 vy = *reinterpret_cast<const float4*>(erb + a.lay.oY + jc);
+            o.a2v[4 * h + 0] = ok ? va.x : 0.f; o.a2v[4 * h + 1] = ok ? va.y : 0.f;
+            o.a2v[4 * h + 2] = ok ? va.z : 0.f; o.a2v[4 * h + 3] = ok ? va.w : 0.f;
+            o.yv[4 * h + 0] = ok ? vy.x : 0.f; o.yv[4 * h + 1] = ok ? vy.y : 0.f;
+            o.yv[4 * h + 2] = ok ? vy.z : 0.f; o.yv[4 * h + 3] = ok ? vy.w : 0.f;
+        }
+        const int ib = i0 + (g >> 1);
+#pragma unroll
+        for (int ks = 0; ks < RAE_MT_NKS; ++ks) {
+            const int q = min(ib + 2 * ks, r - 1);
+            const float lx = erb[a.lay.oX + q], lc = erb[a.lay.oA1 + q];
+            const bool ok = bv && ib + 2 * ks < r;
+            o.xq[ks] = ok ? lx : 0.f;
+            o.cq[ks] = ok ? lc : 0.f;
+        }
+    };
     bool first = true;
     for (int bt = w; bt < nbt || first; bt += RAE_MTW) {
         const bool has = bt < nbt;
@@ -420,7 +454,8 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
             wacc.w += cw[ii] * acc[3];
         }
         RAE_MT_STAMP(4);
-        // cv side: sum over the four lane groups g (fixed order); groups 0, 1 write i0 + 4g..+3
+        // cv side: sum over the four lane groups g (fixed order); groups g < RAE_MTI / 4 write
+        // i0 + 4g .. +3
 #pragma unroll
         for (int ii = 0; ii < RAE_MTI; ++ii) {
             vp[ii] += __uint_as_float(xor16_u32(__float_as_uint(vp[ii])));
@@ -428,12 +463,11 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
         }
         if (bv) {
             float* vo = a.mtV + ((int64_t)jt * l + bb) * a.r4 + i0 + 4 * g;
-            if (g < 2 && i0 + 4 * g < r) {
-                float4 o;
-                o.x = g == 0 ? vp[0] : vp[4];
-                o.y = g == 0 ? vp[1] : vp[5];
-                o.z = g == 0 ? vp[2] : vp[6];
-                o.w = g == 0 ? vp[3] : vp[7];
+            if (4 * g < RAE_MTI && i0 + 4 * g < r) {
+                float4 o = make_float4(vp[0], vp[1], vp[2], vp[3]);
+#pragma unroll
+                for (int q = 1; q < RAE_MTI / 4; ++q)
+                    if (g == q) o = make_float4(vp[4 * q], vp[4 * q + 1], vp[4 * q + 2], vp[4 * q + 3]);
                 *reinterpret_cast<float4*>(vo) = o;
             }
             if (j0 + 4 * g < r)
@@ -441,51 +475,27 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
         }
         RAE_MT_STAMP(5);
         if constexpr (BF16) {
-            if (pass == 1 && a.mtP) {
+            if (dpass) {
                 // the block's share of dP_b[k] = sum_ij U_b[i][j] R[i][j][k], U = x a2^T + a1 y^T,
                 // from the same staged block (k_bil_dp2's contraction without another read of
-                // R): D[b][k] over K = the block's 128 (i, j) pairs = its LDS rows; A = U (lane
+                // R): D[b][k] over K = the block's 16 RAE_MTI (i, j) pairs = its LDS rows; A = U (lane
                 // (li, g): example bb, pairs 32 ks + 8g .. +7 = row i0 + 2 ks + g/2, columns
                 // j0 + 8 (g&1) .. +7), B = 8 rows of the LDS image at column k
-                const int jh = j0 + 8 * (g & 1);
-                float a2v[8], yv[8];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int j = jh + 4 * h;                // r4 padding of the record is zero
-                    const bool ok = bv && j < r;
-                    const int jc = j < r ? j : 0;
-                    const float4 va = *reinterpret_cast<const float4*>(erb + a.lay.oA2 + jc);
-                    const float4 vy = *reinterpret_cast<const float4*>(erb + a.lay.oY + jc);
-                    a2v[4 * h + 0] = ok ? va.x : 0.f; a2v[4 * h + 1] = ok ? va.y : 0.f;
-                    a2v[4 * h + 2] = ok ? va.z : 0.f; a2v[4 * h + 3] = ok ? va.w : 0.f;
-                    yv[4 * h + 0] = ok ? vy.x : 0.f; yv[4 * h + 1] = ok ? vy.y : 0.f;
-                    yv[4 * h + 2] = ok ? vy.z : 0.f; yv[4 * h + 3] = ok ? vy.w : 0.f;
-                }
-                // x / a1 at rows i0 + 2 ks + g/2, ks = 0..3 (named: the K-step loop is rolled)
-                // (unconditional loads of clamped addresses, then selects: a conditional load
-                // becomes a flat load through a zeroed scratch slot)
-                const int ib = i0 + (g >> 1);
-                const float* px = erb + a.lay.oX;
-                const float* pc = erb + a.lay.oA1;
-                const int q0 = min(ib, r - 1), q1 = min(ib + 2, r - 1), q2 = min(ib + 4, r - 1),
-                          q3 = min(ib + 6, r - 1);
-                const float lx0 = px[q0], lx1 = px[q1], lx2 = px[q2], lx3 = px[q3];
-                const float lc0 = pc[q0], lc1 = pc[q1], lc2 = pc[q2], lc3 = pc[q3];
-                const float x0 = (bv && ib < r) ? lx0 : 0.f, c0 = (bv && ib < r) ? lc0 : 0.f;
-                const float x1 = (bv && ib + 2 < r) ? lx1 : 0.f, c1 = (bv && ib + 2 < r) ? lc1 : 0.f;
-                const float x2 = (bv && ib + 4 < r) ? lx2 : 0.f, c2 = (bv && ib + 4 < r) ? lc2 : 0.f;
-                const float x3 = (bv && ib + 6 < r) ? lx3 : 0.f, c3 = (bv && ib + 6 < r) ? lc3 : 0.f;
+                DpOps dop;
+                load_dp(dop, erb, bv);
                 const int nkt = (m + 15) / 16;               // <= 8 (m <= 128)
                 rae_bf4 dacc[8];
 #pragma unroll
                 for (int kt = 0; kt < 8; ++kt) dacc[kt] = rae_bf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-                for (int ks = 0; ks < 4; ++ks) {             // rolled: one K step's fragments live
-                    const float xk = (ks & 2) ? ((ks & 1) ? x3 : x2) : ((ks & 1) ? x1 : x0);
-                    const float ak = (ks & 2) ? ((ks & 1) ? c3 : c2) : ((ks & 1) ? c1 : c0);
+                for (int ks = 0; ks < RAE_MT_NKS; ++ks) {    // rolled: one K step's fragments live
+                    float xk = dop.xq[0], ak = dop.cq[0];    // selects, not a dynamic index
+#pragma unroll
+                    for (int t = 1; t < RAE_MT_NKS; ++t)
+                        if (ks == t) { xk = dop.xq[t]; ak = dop.cq[t]; }
                     rae_bf16x8 ua;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) ua[e] = (__bf16)(xk * a2v[e] + ak * yv[e]);
+                    for (int e = 0; e < 8; ++e) ua[e] = (__bf16)(xk * dop.a2v[e] + ak * dop.yv[e]);
                     // B[pair][k]: the transposed image, 8 consecutive pairs at column k
                     const __bf16* lt = sT + li * RAE_MT_TP + ks * 32 + 8 * g;
 #pragma unroll
@@ -508,6 +518,7 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                             a.mtP[((int64_t)blockIdx.x * l + bo) * m + k] = dacc[kt][reg];
                     }
                 }
+                RAE_MT_STAMP(7);
             }
         }
     }

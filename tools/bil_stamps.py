@@ -50,7 +50,7 @@ def main():
     per = []
     vw = []
     nvw = ((cfg["r"] + 7) // 8) * ((cfg["r"] + 15) // 16)
-    NSLOT = 7 if "RAE_MT_STAMP_PASS=1" in os.environ.get("RAE_VARIANT", "") else 6
+    NSLOT = 8 if "RAE_MT_STAMP_PASS=1" in os.environ.get("RAE_VARIANT", "") else 6
     for it in range(args.iters):
         bf = torch.zeros(16384 + nvw * 8, dtype=torch.int64, device=dev)
         lib.rae_debug_stamps(eng.plan, C.c_void_p(bf.data_ptr()), 1)
@@ -78,10 +78,14 @@ def main():
         print(f"  late WGs (> 5 us) by blockIdx: {sorted(set(late.tolist()))[:40]} ... (XCD = blockIdx % 8: "
               f"{np.bincount(late % 8, minlength=8).tolist()})")
     vw = np.concatenate(vw)
-    vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write", "dP"][:NSLOT]
-    print(f"k_bil_mt pass {1 if NSLOT == 7 else 0} ({nvw} workgroups, wave 0 of each), median/max us per phase:")
+    vcols = ["start", "staging", "operand loads", "barrier", "MFMA+contraction", "write", "dP",
+             "dP stores"][:NSLOT]
+    print(f"k_bil_mt pass {1 if NSLOT == 8 else 0} ({nvw} workgroups, wave 0 of each), median/max us per phase:")
     print("  " + "  ".join(f"{c} {np.median(vw[:, i]):.2f}/{vw[:, i].max():.2f}"
                            for i, c in enumerate(vcols)))
+    end = vw.sum(axis=1)                          # wave 0's last stamp after the first WG start
+    print("  wave-0 end after the first start, p10/p50/p90/p99/max us: " +
+          "/".join(f"{np.percentile(end, q):.2f}" for q in (10, 50, 90, 99)) + f"/{end.max():.2f}")
 
 
 if __name__ == "__main__":
