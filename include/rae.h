@@ -87,6 +87,7 @@ typedef struct rae_config {
     int32_t bil_dp;           /* bilinear dCost/dP contraction: RAE_BILDP_*                 */
     int32_t bil_prep;         /* bf16 R-gradient operands: RAE_BILPREP_*                    */
     int32_t dp_update;        /* data-parallel update: RAE_DPUPD_*                          */
+    int32_t priv_rows;        /* rows one record of the batch references: RAE_PRIV_*        */
 } rae_config;
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
@@ -102,6 +103,12 @@ typedef struct rae_config {
                                 * replicas after every step)                                  */
 #define RAE_DPUPD_PARTITIONED 1 /* rank k updates the rows it owns (row % G == k) and pushes *
                                  * the next step's rows to the ranks that read them            */
+#define RAE_PRIV_AUTO 0       /* single-rank SP plans on the compile-time-shape forward (C3): a  *
+                               * row exactly one record of the global batch references is     *
+                               * updated by that example's forward workgroup, the update       *
+                               * launch keeps the shared rows and the dense tiles (same        *
+                               * arithmetic, bit-identical parameters)                         */
+#define RAE_PRIV_OFF 1        /* every row updated by the update launch                        */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]
@@ -143,7 +150,7 @@ int64_t rae_exchange_record_floats(const rae_config* cfg);
 int64_t rae_exchange_floats(const rae_config* cfg);
 
 /* The kernel forms the plan resolved for its shape (RAE_SPFWD_FUSED / _SPLIT, RAE_BILDP_*,
- * RAE_BILPREP_*, RAE_DPUPD_*; 0 where a form does not apply to the decoder), written into
+ * RAE_BILPREP_*, RAE_DPUPD_*, RAE_PRIV_*; 0 where a form does not apply to the decoder), written into
  * the matching fields of *out (the other fields are left as they are).                  */
 int rae_plan_forms(const rae_plan* plan, rae_config* out);
 

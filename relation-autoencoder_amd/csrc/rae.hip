@@ -212,12 +212,25 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_UPD_WGCAP
 #define RAE_UPD_WGCAP 6144    // row-task workgroups (grid-stride beyond; 1536 = one resident round)
 #endif
-__host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC) {
+#ifndef RAE_PRIV_LAST
+#define RAE_PRIV_LAST 1       // private-row workgroups dispatched after every other update task
+#endif
+#ifndef RAE_PRIV_ROWW
+#define RAE_PRIV_ROWW 4       // private rows: row-task waves per example of the global batch
+#endif
+__host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC, int L,
+                                               int priv) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
     const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
     int64_t rows = ((int64_t)TC * RAE_ROWPCT / 100 + RAE_NWAVE - 1) / RAE_NWAVE;
+    // with the private rows (StepArgs::priv) taken per example by leading workgroups, the
+    // dispatch table keeps ~5 % of the rows: a smaller row grid, grid-striding when a batch has more
+    if (priv) {
+        const int64_t pr = ((int64_t)L * RAE_PRIV_ROWW + RAE_NWAVE - 1) / RAE_NWAVE;
+        if (pr < rows) rows = pr;
+    }
     if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
-    return (int64_t)nT + nP + NVC + rows;
+    return (int64_t)nT + nP + NVC + rows + (priv ? (RAE_PRA + 1ll) * L : 0);
 }
 
 // LDS of one update workgroup: workgroup tasks' partials (a row: Q vectors per lane, or a tile:
@@ -241,9 +254,19 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
     // record offset derived from them is then scalar (s_load of the segment, SGPR soffsets,
     // scalar branches) instead of VGPR-resident and exec-masked
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wgp = __builtin_amdgcn_readfirstlane(wg0);
+    int wgp = __builtin_amdgcn_readfirstlane(wg0);
     const int gw = wgp * RAE_NWAVE + w;
     const int64_t g = step_batch(a);
+    if (a.priv) {                 // private rows: (RAE_PRA + 1) L workgroups, dispatched
+        const int nX = (RAE_PRA + 1) * a.L;       // first (RAE_PRIV_LAST 0) or last
+        const int x = RAE_PRIV_LAST ? wgp - (ngrid - nX) : wgp;
+        if (x >= 0 && x < nX) {
+            task_private_rows<OPT, V4, Q, BIL>(a, g, x, w, lane);
+            return;
+        }
+        if (!RAE_PRIV_LAST) wgp -= nX;
+        ngrid -= nX;
+    }
     const int64_t ex0 = g * (int64_t)a.L;
     const int mt = (a.m + 15) / 16, rt = (a.r + 15) / 16;
     const int nCt = n_ctiles(a.dec, a.r, a.m);
@@ -577,8 +600,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     if (c.sp_forward < RAE_SPFWD_AUTO || c.sp_forward > RAE_SPFWD_SPLIT ||
         c.bil_dp < RAE_BILDP_AUTO || c.bil_dp > RAE_BILDP_MTILE ||
         c.bil_prep < RAE_BILPREP_AUTO || c.bil_prep > RAE_BILPREP_KERNEL ||
-        c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED)
-        return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update)");
+        c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED ||
+        c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_OFF)
+        return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
+                                   "priv_rows)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -760,6 +785,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                            (c.sp_forward == RAE_SPFWD_AUTO &&
                             (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
     const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
+    // private rows (rows one record of the batch references, updated per example): single-rank
+    // plans without a regulariser (a row then changes only through its records); the example's
+    // record slots in one wave (NJ <= 64), its features from the descriptor (<= dcap, <= 32)
+    a.priv = (c.world_size == 1 && !a.reg_on && NJ <= 64 && c.priv_rows == RAE_PRIV_AUTO) ? 1 : 0;
+    a.privnf = a.priv ? (a.dcap < 32 ? a.dcap : 32) : 0;
+    const size_t o_pmask = a.priv ? take(16ull * W_ * c.batch_size) : 0;
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
@@ -802,6 +833,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.dpl = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpl) : nullptr;
     a.dpc = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpc) : nullptr;
     a.dpmax = reinterpret_cast<int*>(p->ws + o_dpm);
+    a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -824,7 +856,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                    "workgroup (relations / embed / neg_samples too large)");
     }
     p->grid_fwd = c.batch_size;
-    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC);
+    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC, L, a.priv);
     if (gu >= (1ll << 31)) {
         (void)hipFree(p->ws);
         delete p;
@@ -881,6 +913,7 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
     out->bil_prep = (!bil || !p->args.bf16) ? 0 : (p->args.fuse_prep ? RAE_BILPREP_AUTO
                                                                     : RAE_BILPREP_KERNEL);
     out->dp_update = p->cfg.dp_update;
+    out->priv_rows = p->args.priv ? RAE_PRIV_AUTO : RAE_PRIV_OFF;
     return RAE_OK;
 }
 

@@ -166,8 +166,23 @@ __device__ __forceinline__ float opt_update(float p, float* acc, float g, float 
         *acc = a;
         return p - (lr * g) / (sqrtf(a) + 1e-6f);
     } else {
-        return p - lr * g;
+        // one rounding, spelled out: left to fp-contract, the fused and the unfused forms of
+        // p - lr g differ in the last bit near cancellation, and the two kernels that apply
+        // SGD (k_update, the forward's private rows) must agree bit for bit
+        return __builtin_fmaf(-lr, g, p);
     }
+}
+
+template <int OPT>
+__device__ __forceinline__ void updv(float& p, float& ac, float g, float lr) {
+    p = opt_update<OPT>(p, &ac, g, lr);
+}
+template <int OPT>
+__device__ __forceinline__ void updv(float4& p, float4& ac, float4 g, float lr) {
+    p.x = opt_update<OPT>(p.x, &ac.x, g.x, lr);
+    p.y = opt_update<OPT>(p.y, &ac.y, g.y, lr);
+    p.z = opt_update<OPT>(p.z, &ac.z, g.z, lr);
+    p.w = opt_update<OPT>(p.w, &ac.w, g.w, lr);
 }
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) - (x < 0.f); }

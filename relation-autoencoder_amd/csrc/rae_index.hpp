@@ -99,6 +99,10 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
     int4* vseg = reinterpret_cast<int4*>(isA ? a.vrowA : a.vrowW) + slot * (int64_t)Vcap;
     if (!isA)
         for (int b = tid; b <= a.L; b += BT) sptr[b] = a.indptr[ex0 + b];
+    if (a.priv) {                // private-row masks of this batch: A words 0, 1 / W words 2, 3
+        int2* pm = reinterpret_cast<int2*>(a.pmask + slot * (int64_t)a.L * 4) + (isA ? 0 : 1);
+        for (int b = tid; b < a.L; b += BT) pm[2 * b] = make_int2(0, 0);
+    }
     __syncthreads();
     const int P0 = isA ? 0 : sptr[0];
     const int nrec = isA ? a.L * NJ : sptr[a.L] - P0;
@@ -183,18 +187,38 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
                 st = sstart[v];
                 en = (v + 1 < nu) ? sstart[v + 1] : cnt;
             }
+            // private row (StepArgs::priv): one record, of an example whose features the
+            // descriptor holds (at most privnf) -- the update's per-example workgroups take it
+            // (SP: e2's rows, with no A gradient, stay in the table)
+            bool psg = false;
+            if (a.priv && valid && en - st == 1) {
+                const unsigned rec = (unsigned)(keys[st] & 0xffffffffull);
+                if (isA) {
+                    const int b = (int)(rec / (unsigned)NJ), j = (int)rec - b * NJ;
+                    psg = (j != 1 || a.dec != 0) && a.indptr[ex0 + b + 1] - a.indptr[ex0 + b] <= a.privnf;
+                    if (psg) atomicOr(a.pmask + (slot * a.L + b) * 4 + (j >> 5), 1 << (j & 31));
+                } else {
+                    const int b = (int)(rec >> a.posbits);
+                    const int pos = (int)(rec & ((1u << a.posbits) - 1u));
+                    psg = sptr[b + 1] - sptr[b] <= a.privnf;
+                    if (psg) atomicOr(a.pmask + (slot * a.L + b) * 4 + 2, 1 << pos);
+                }
+            }
+#ifdef RAE_DIAG_NOSINGLE      // timing knockout (wrong results): rows with one record are skipped
+            psg = psg || (valid && en - st == 1);
+#endif
             const bool vheavy = valid && (en - st) > RAE_VHEAVY;
             const bool heavy = valid && !vheavy && (en - st) > RAE_HEAVY;
             int htot, ltot, vtot;
             const int hp = block_flag_scan<BT>(heavy, sint + 1, &htot);
-            const int lp = block_flag_scan<BT>(valid && (en - st) <= RAE_HEAVY, sint + 12, &ltot);
+            const int lp = block_flag_scan<BT>(valid && !psg && (en - st) <= RAE_HEAVY, sint + 12, &ltot);
             const int vp = block_flag_scan<BT>(vheavy, sint + 21, &vtot);
             if (valid) {
                 const unsigned long long k = keys[st];
                 const int4 sg = make_int4((int)(unsigned)(k >> 32), base_i + st, base_i + en,
                                           (int)(unsigned)(k & 0xffffffffull));
                 if (vheavy) vseg[nv + vp] = sg;
-                else seg[heavy ? nh + hp : Rcap - 1 - (nl + lp)] = sg;
+                else if (!psg) seg[heavy ? nh + hp : Rcap - 1 - (nl + lp)] = sg;
             }
             nh += htot;
             nl += ltot;

@@ -131,6 +131,12 @@ struct StepArgs {
     int capA, capW;      // rows per peer block (set with the buffers; <= LA / LW)
     int64_t dblk;
     int* dpmax;          // longest list built since the last rae_dp_list_max [entity, feature]
+    // private rows: rows a single record of the global batch references (rae.h RAE_PRIV_AUTO;
+    // single-rank SP plans), updated per example by the update launch's leading workgroups;
+    // pmask per slot and example = (entity-slot bits j < 32, j >= 32, feature-position bits,
+    // 0); the row index leaves these rows out of the update's dispatch table
+    int priv, privnf;    // enabled; longest feature row whose rows may be private
+    int32_t* pmask;
     unsigned long long* stamps;   // diagnostic build only (RAE_STAMPS): phase timestamps
 };
 
@@ -141,6 +147,9 @@ __device__ __forceinline__ int64_t step_batch(const StepArgs& a) {
     return a.cursor ? *a.cursor + a.step_offset : a.step_offset;
 }
 
+#if defined(RAE_DIAG_NOSINGLE) && !defined(RAE_DIAG)
+#error "RAE_DIAG_NOSINGLE is a timing knockout with wrong results: a diagnostic build (-DRAE_DIAG)"
+#endif
 #if defined(RAE_STAMPS) && !defined(RAE_DIAG)
 #error "RAE_STAMPS instruments the kernels for tools/phase_stamps.py: a diagnostic build (-DRAE_DIAG)"
 #endif

@@ -200,17 +200,6 @@ struct RowVec {
     }
 };
 
-template <int OPT>
-__device__ __forceinline__ void updv(float& p, float& ac, float g, float lr) {
-    p = opt_update<OPT>(p, &ac, g, lr);
-}
-template <int OPT>
-__device__ __forceinline__ void updv(float4& p, float4& ac, float4 g, float lr) {
-    p.x = opt_update<OPT>(p.x, &ac.x, g.x, lr);
-    p.y = opt_update<OPT>(p.y, &ac.y, g.y, lr);
-    p.z = opt_update<OPT>(p.z, &ac.z, g.z, lr);
-    p.w = opt_update<OPT>(p.w, &ac.w, g.w, lr);
-}
 
 template <int OPT, bool V4, int Q>
 __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& pv,
@@ -497,6 +486,128 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
             for (int ww = 1; ww < RAE_NWAVE; ++ww) vadd(g.v[q], spart[(ww * Q + q) * RAE_WAVE + lane]);
         }
         feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
+    }
+}
+
+// ---- private rows (StepArgs::priv): per example, the rows only its own records reference ----
+// The row index (rae_index.hpp) marks a row that exactly one record of the global batch
+// references -- ~95 % of the A rows and ~90 % of the W rows at C3 -- in the example's pmask and
+// leaves it out of the dispatch table.  RAE_PRA + 1 workgroups per example take them: the first
+// RAE_PRA its A / Ab rows (wave i of them the marked rows i, i + 4 RAE_PRA, ...), the last its W
+// rows (wave w: marked features w, w + 4, ...).  A row j's gradient is its one
+// record's c_j vec_j (Ab: gamma_j), a W row's x_f dS_b: k_update's one-record row task, the same
+// arithmetic and stores, so the parameters are bit-identical to the per-row tasks these replace.
+// The loads are batched: one round trip for the example's descriptor ids, coefficients and
+// record vectors (no task entry, no segment), one for a round of up to PRMAX rows.
+#ifndef RAE_PRMAX
+#define RAE_PRMAX 3          // rows per round of one wave (the update kernel's 80-VGPR budget)
+#endif
+#ifndef RAE_PRA
+#define RAE_PRA 4            // workgroups per example for its A rows (+ 1 for its W rows)
+#endif
+template <int OPT, bool V4, int Q, bool XY>
+__device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    constexpr int PRM = Q == 1 ? RAE_PRMAX : RAE_PRMAX / 2;
+    const int b = t / (RAE_PRA + 1), sub = t - b * (RAE_PRA + 1);
+    const int64_t slot = g % a.index_window;
+    const int4 pm = reinterpret_cast<const int4*>(a.pmask)[slot * a.L + b];
+    const int32_t* dsc = a.desc + (slot * a.l + b) * (int64_t)a.dstride;      // G == 1: l == L
+    const float* rec = a.ex + (int64_t)b * a.lay.rec;
+    if (sub < RAE_PRA) {                                      // A / Ab rows
+        const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
+        // record j's entity id and coefficients (c_j, gamma_j) in lane j (NJ <= 64: plan)
+        const int sid = dsc[2 + (lane < NJ ? lane : 0)];
+        const float2 cg = reinterpret_cast<const float2*>(rec + a.lay.ocoef)[lane < NJ ? lane : 0];
+        // record vector of slot j: vec_0 = G1, vec_1 = G2 (bilinear) / V1, neg1 V1, neg2 V2
+        const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;
+        const RecBuf rb_(a.ex);
+        const int rb0 = b * a.lay.rec;
+        // this wave's rows: marked bits wi, wi + 4 RAE_PRA, ... (wi = sub * 4 + w)
+        uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
+        for (int i = 0; i < sub * RAE_NWAVE + w; ++i) M &= M - 1;
+        while (M) {
+            int jr[PRM];
+            RowVec<V4, Q> pv[PRM], av[PRM], vv[PRM];
+            float ab[PRM], aab[PRM];
+#pragma unroll
+            for (int k = 0; k < PRM; ++k) {                   // a round: every load issued first
+                jr[k] = M ? __builtin_ctzll(M) : -1;
+#pragma unroll
+                for (int i = 0; i < RAE_NWAVE * RAE_PRA; ++i) M &= M - 1;
+                if (jr[k] < 0) continue;
+                const int j = jr[k];
+                const int64_t e = __builtin_amdgcn_readlane(sid, j);
+                pv[k].load(a.A + e * r, nv, lane);
+                if (OPT == 0) av[k].load(a.aA + e * r, nv, lane); else av[k].zero();
+                const int vo = rb0 + (j == 0 ? a.lay.oG1 : (j == 1 ? vo1 : (j < 2 + s ? a.lay.oV1 : a.lay.oV2)));
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const int c = lane + RAE_WAVE * q;
+                    rb_.load(vv[k].v[q], (c < nv ? c : 0) * VW, vo);
+                }
+                ab[k] = a.Ab[e];
+                aab[k] = (OPT == 0) ? a.aAb[e] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < PRM; ++k) {
+                const int j = jr[k];
+                if (j < 0) continue;
+                const int64_t e = __builtin_amdgcn_readlane(sid, j);
+                const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.x), j));
+                const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.y), j));
+                RowVec<V4, Q> gr;
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    vzero(gr.v[q]);
+                    vfma(gr.v[q], cj, vv[k].v[q]);
+                }
+                apply_row<OPT, V4, Q>(a.A + e * r, (OPT == 0) ? a.aA + e * r : nullptr, pv[k], av[k],
+                                      gr, nv, a.lr, lane);
+                if (lane == 0) ab_update<OPT>(a, (int)e, ab[k], aab[k], gj);
+            }
+        }
+    } else {                                                  // W rows
+        const int NJ = 2 + 2 * a.s, m = a.m, nv = m / VW;
+        const int nf = dsc[0], p0 = dsc[1];
+        const int fid = dsc[2 + NJ + (lane < 32 ? lane : 0)];   // features 0..31 (privnf <= dcap)
+        typedef typename VecT<V4>::T VT;
+        const VT* rv = reinterpret_cast<const VT*>(rec);
+        VT ds[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int c = lane + RAE_WAVE * q;
+            ds[q] = rv[a.lay.odS / VW + (c < nv ? c : 0)];
+        }
+        unsigned M = (unsigned)pm.z;
+        for (int i = 0; i < w; ++i) M &= M - 1;
+        (void)nf;
+        while (M) {
+            int fr[PRM];
+            RowVec<V4, Q> pv[PRM], av[PRM];
+            float xv[PRM];
+#pragma unroll
+            for (int k = 0; k < PRM; ++k) {
+                fr[k] = M ? __builtin_ctz(M) : -1;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) M &= M - 1;
+                if (fr[k] < 0) continue;
+                const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
+                pv[k].load(a.W + f * m, nv, lane);
+                if (OPT == 0) av[k].load(a.aW + f * m, nv, lane); else av[k].zero();
+                xv[k] = a.values ? a.values[p0 + fr[k]] : 1.f;
+            }
+#pragma unroll
+            for (int k = 0; k < PRM; ++k) {
+                if (fr[k] < 0) continue;
+                const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
+                RowVec<V4, Q> gr;
+#pragma unroll
+                for (int q = 0; q < Q; ++q) { vzero(gr.v[q]); vfma(gr.v[q], xv[k], ds[q]); }
+                apply_row<OPT, V4, Q>(a.W + f * m, (OPT == 0) ? a.aW + f * m : nullptr, pv[k], av[k],
+                                      gr, nv, a.lr, lane);
+            }
+        }
     }
 }
 

@@ -240,7 +240,8 @@ class TrainEngine:
     def kernel_forms_in_use(self):
         """The kernel forms the plan resolved for its shape (rae_plan_forms): sp_forward
         fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep fused|kernel
-        (bf16 bilinear), dp_update; None where a form does not apply."""
+        (bf16 bilinear), dp_update, priv_rows forward|off (rows one record references
+        updated by the forward); None where a form does not apply."""
         out = _lib.RaeConfig()
         _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
         F = _lib.KERNEL_FORMS
@@ -250,7 +251,8 @@ class TrainEngine:
         return {"sp_forward": name["sp_forward"][out.sp_forward] if sp else None,
                 "bil_dp": name["bil_dp"][out.bil_dp] if not sp else None,
                 "bil_prep": ("kernel" if out.bil_prep == 1 else "fused") if bf16 else None,
-                "dp_update": name["dp_update"][out.dp_update]}
+                "dp_update": name["dp_update"][out.dp_update],
+                "priv_rows": "forward" if out.priv_rows == 0 else "off"}
 
     def _moves(self):
         return int(self.lib.rae_cursor_moves(self.plan))

@@ -546,6 +546,35 @@ def test_fast_paths_ragged_vs_oracle(built_lib, cuda_dev, dec):
     _assert_params_close(_params(ind), tr.params, "ragged-fast")
 
 
+@pytest.mark.parametrize("opt,values", [("adagrad", False), ("sgd", False), ("adagrad", True)])
+def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values):
+    """Rows one record of the batch references, updated by the example's forward workgroup
+    (rae.h RAE_PRIV_AUTO, C3's compile-time-shape forward), train bit-identically to the update
+    launch doing every row (priv_rows=off): same parameters, accumulators and costs."""
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    out = []
+    for form in ("auto", "off"):
+        data, gold = synthetic_dataset(400, 3000, 10, seed=21)
+        if values:                                   # non-binary features: x_f != 1
+            x = data.split["train"].xFeats
+            x.data = np.random.RandomState(5).uniform(0.5, 2.0, size=x.data.shape).astype(np.float32)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 100, 200, 100, 20,
+                                 0.0, 0.0, opt, "priv", "sp", False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, kernel_forms={"priv_rows": form})
+        ind.compile_function()
+        assert ind.engine.kernel_forms_in_use()["priv_rows"] == ("forward" if form == "auto" else "off")
+        ind.learn(verbose=False)
+        acc = {}
+        if ind.optimizer.accumulator is not None:
+            acc = {f"acc_{k}": v.detach().cpu().numpy().copy()
+                   for k, v in zip(ind.modelFunc.param_names, ind.optimizer.accumulator)}
+        out.append(({**_params(ind), **acc}, np.array(ind.epoch_costs)))
+    for k in out[0][0]:
+        assert np.array_equal(out[0][0][k], out[1][0][k]), k
+    assert np.array_equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("m", [12, 100, 300, 7])      # 16 / 32 / 64 lanes per row; scalar path
 def test_label_pass_every_row_length(built_lib, cuda_dev, m):
     """rae_label on rows of every length 0..130 (each length ten times): the lane-group

@@ -29,11 +29,11 @@ def _rows(d):
 def _group(name):
     n = name.split("(")[0].replace("void ", "").strip()
     base = n.split("<")[0]
-    if base == "k_forward" or base in ("k_bil_enc", "k_bil_mt", "k_bil_dec", "k_bil_dp", "k_bil_dp2",
+    if base == "k_forward" or base in ("k_bil_enc", "k_bil_enc_fast", "k_bil_mt", "k_bil_dec", "k_bil_dp", "k_bil_dp2",
                                        "k_bil_fin", "k_sp_enc", "k_sp_cp", "k_sp_dec", "k_sp_ctdw",
                                        "k_sp_fin"):
         return "k_forward", base
-    if base in ("k_update", "k_update_bil", "k_bil_prep", "k_bil_rows", "k_dense_w",
+    if base in ("k_update", "k_update_bil", "k_bil_update", "k_bil_prep", "k_bil_rows", "k_dense_w",
                 "k_finalize_cost"):
         return "k_update", base
     return None, base
