@@ -77,8 +77,13 @@ __device__ void lds_bitonic_sort(unsigned long long* keys, int n2) {
     }
 }
 
+// records per partition (hash of the row): the bitonic sort's length is the next power of two
+// of a partition's records, so ~RAE_IDX_PART keys per partition keep the padding small
+#ifndef RAE_IDX_PART
+#define RAE_IDX_PART 1024      // measured at C3: 4096 -> 0.98, 2048 -> 0.83, 1024 -> 0.79 us per batch
+#endif
 __host__ __device__ inline int index_partitions(int nrec) {
-    return nrec <= RAE_KCAP / 2 ? 1 : (nrec + RAE_KCAP / 2 - 1) / (RAE_KCAP / 2);
+    return nrec <= RAE_IDX_PART ? 1 : (nrec + RAE_IDX_PART - 1) / RAE_IDX_PART;
 }
 
 template <int BT>

@@ -162,11 +162,10 @@ class TrainEngine:
                    "rae_plan_create")
         self.plan = handle
         self.index_window = int(self.lib.rae_index_window(self.plan))
-        # a batch with more records than one LDS sort holds (RAE_KCAP / 2 = 4096, rae_common.hpp)
-        # is hash-partitioned, and a partition can overflow (a Zipf-heavy row at a large global
-        # batch): then run() checks the device error word after building each window's index,
-        # before any step of the window applies an update
-        self._index_partitioned = self.L * (2 + 2 * self.s) > 4096 or mbn > 4096
+        # a batch's row index is hash-partitioned (rae_index.hpp RAE_IDX_PART records per
+        # partition) and a partition can overflow its LDS sort (a Zipf-heavy row at a large global
+        # batch): run() checks the device error word after building each window's index, before
+        # any step of the window applies an update (one host sync per window)
         self._graphs = {}
         self._epoch_mode = None
         # graph_absolute: every captured step carries its absolute batch index in the launch
@@ -479,8 +478,7 @@ class TrainEngine:
             if index:
                 _lib.check(self.lib.rae_build_index(self.plan, b, n, self._stream()),
                            "rae_build_index")
-                if self._index_partitioned or self._dp:
-                    self.check()
+                self.check()
                 if self._dp:
                     self._dp_caps_check()
             if graph and self.graph_chunk > 1 and self.graph_absolute:
