@@ -56,20 +56,21 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* ws, int* total) {
     return off + pre;
 }
 
+// Bitonic sort of n2 (a power of two) 64-bit keys in LDS: one compare-exchange pair (i, i + j)
+// per thread and step (pair p -> i with bit j clear), a workgroup barrier per step.  (Running
+// the steps whose pairs stay inside one wave's block without the barrier measured no faster.)
 template <int BT>
 __device__ void lds_bitonic_sort(unsigned long long* keys, int n2) {
     const int tid = threadIdx.x;
     for (int k = 2; k <= n2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < n2; i += BT) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = keys[i], y = keys[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((x > y) == up) {
-                        keys[i] = y;
-                        keys[ixj] = x;
-                    }
+            for (int p = tid; p < (n2 >> 1); p += BT) {
+                const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), ixj = i + j;
+                const unsigned long long x = keys[i], y = keys[ixj];
+                const bool up = (i & k) == 0;
+                if ((x > y) == up) {
+                    keys[i] = y;
+                    keys[ixj] = x;
                 }
             }
             __syncthreads();
