@@ -23,3 +23,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- p
 cut -c1-110 $O/prof/run_kernel_stats.csv | head -8
 cd $R
 K=none CFG=c5 bash tools/gpu_s5.sh $TAG/c5 || exit 1
+timeout -k 10 300 python3 -u bench.py --config c5 --no-cpu-baseline --no-label-pass --steps 256 --kernel-form priv_rows=off > $O/bench_c5_privoff.json 2> $O/bench_c5_privoff.err || { echo c5 privoff bench failed; tail -20 $O/bench_c5_privoff.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_c5_privoff.json')); print('c5 priv_rows=off', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: round(v, 2) for k, v in d['kernel_us'].items()})"
