@@ -251,7 +251,7 @@ class TrainEngine:
                 "bil_dp": name["bil_dp"][out.bil_dp] if not sp else None,
                 "bil_prep": ("kernel" if out.bil_prep == 1 else "fused") if bf16 else None,
                 "dp_update": name["dp_update"][out.dp_update],
-                "priv_rows": "forward" if out.priv_rows == 0 else "off"}
+                "priv_rows": "per_example" if out.priv_rows == 0 else "off"}
 
     def _moves(self):
         return int(self.lib.rae_cursor_moves(self.plan))

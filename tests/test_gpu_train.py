@@ -548,9 +548,10 @@ def test_fast_paths_ragged_vs_oracle(built_lib, cuda_dev, dec):
 
 @pytest.mark.parametrize("opt,values", [("adagrad", False), ("sgd", False), ("adagrad", True)])
 def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values):
-    """Rows one record of the batch references, updated by the example's forward workgroup
-    (rae.h RAE_PRIV_AUTO, C3's compile-time-shape forward), train bit-identically to the update
-    launch doing every row (priv_rows=off): same parameters, accumulators and costs."""
+    """Rows one record of the batch references, updated by per-example workgroups of the update
+    launch (rae.h RAE_PRIV_AUTO), train bit-identically to the update launch's row tasks doing
+    every row (priv_rows=off): same parameters, accumulators and costs."""
+    s = 20
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     out = []
@@ -559,11 +560,11 @@ def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values):
         if values:                                   # non-binary features: x_f != 1
             x = data.split["train"].xFeats
             x.data = np.random.RandomState(5).uniform(0.5, 2.0, size=x.data.shape).astype(np.float32)
-        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 100, 200, 100, 20,
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 100, 200, 100, s,
                                  0.0, 0.0, opt, "priv", "sp", False, True, False, 1.0,
                                  device=cuda_dev, graph_chunk=2, kernel_forms={"priv_rows": form})
         ind.compile_function()
-        assert ind.engine.kernel_forms_in_use()["priv_rows"] == ("forward" if form == "auto" else "off")
+        assert ind.engine.kernel_forms_in_use()["priv_rows"] == ("per_example" if form == "auto" else "off")
         ind.learn(verbose=False)
         acc = {}
         if ind.optimizer.accumulator is not None:
