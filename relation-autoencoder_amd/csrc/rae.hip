@@ -36,7 +36,8 @@ using namespace rae;
 
 #define RAE_VERSION 1
 #ifndef RAE_UPD_WPE
-#define RAE_UPD_WPE 6   // SP update: <= 85 VGPRs -> 24 waves per CU, a C3 step's row tasks all resident
+#define RAE_UPD_WPE 5   // SP update: <= 102 VGPRs -> 20 waves per CU (6: 85 VGPRs spilled the
+                        // Q = 2 rows of C4 -- 23.8 vs 20.2 us update; r03_ab.txt)
 #endif
 
 // ======================================================================================

@@ -203,7 +203,7 @@ __device__ __forceinline__ void vfma(float4& acc, float s, float4 v) {
 }
 // Exchange-record loads through one buffer resource: the record's offset rides in the scalar
 // soffset, the lane's column in a 32-bit voffset -- one SGPR per load instead of a 64-bit
-// address pair, which is what lets the update's wide rounds fit its 80-VGPR budget.
+// address pair, which is what lets the update's wide rounds fit its VGPR budget (RAE_UPD_WPE).
 // (dword3 0x00020000: the gfx9-family raw-buffer format word.)
 typedef unsigned rae_v4u __attribute__((ext_vector_type(4)));
 struct RecBuf {

@@ -500,10 +500,10 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
 // The loads are batched: one round trip for the example's descriptor ids, coefficients and
 // record vectors (no task entry, no segment), one for a round of up to PRMAX rows.
 #ifndef RAE_PRMAX
-#define RAE_PRMAX 3          // rows per round of one wave (the update kernel's 80-VGPR budget)
+#define RAE_PRMAX 4          // rows per round of one wave (within the update kernel's VGPR budget)
 #endif
 #ifndef RAE_PRA
-#define RAE_PRA 4            // workgroups per example for its A rows (+ 1 for its W rows)
+#define RAE_PRA 3            // workgroups per example for its A rows (+ 1 for its W rows)
 #endif
 template <int OPT, bool V4, int Q, bool XY>
 __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {

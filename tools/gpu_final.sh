@@ -25,3 +25,7 @@ cd $R
 K=none CFG=c5 bash tools/gpu_s5.sh $TAG/c5 || exit 1
 timeout -k 10 300 python3 -u bench.py --config c5 --no-cpu-baseline --no-label-pass --steps 256 --kernel-form priv_rows=off > $O/bench_c5_privoff.json 2> $O/bench_c5_privoff.err || { echo c5 privoff bench failed; tail -20 $O/bench_c5_privoff.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_c5_privoff.json')); print('c5 priv_rows=off', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: round(v, 2) for k, v in d['kernel_us'].items()})"
+for c in c2 c4; do
+  timeout -k 10 400 python3 -u bench.py --config $c --no-cpu-baseline --no-label-pass > $O/bench_$c.json 2> $O/bench_$c.err || { echo $c bench failed; tail -20 $O/bench_$c.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_$c.json')); print('$c', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: round(v, 2) for k, v in d['kernel_us'].items()})"
+done
