@@ -806,3 +806,62 @@ def test_label_argmax_nan_and_inf_follow_numpy(built_lib, cuda_dev):
     special = ~np.all(np.isfinite(S), axis=1)
     assert special.sum() > 0
     assert np.array_equal(got[special], want[special])
+
+
+def _record_offsets(dec, m, r, s):
+    """The exchange record's field offsets (rae_step.hpp make_layout: P, dS, V1, V2, dw1, dw2,
+    G1, [G2, X, Y, A1, A2, Z, aux,] coefficients, loss; m and r padded to multiples of 4)."""
+    a4 = lambda x: (x + 3) & ~3
+    m4, r4 = a4(m), a4(r)
+    o = {"P": 0, "V1": 2 * m4, "V2": 2 * m4 + r4}
+    end = 2 * m4 + 5 * r4
+    if dec != "sp":
+        end += 5 * r4 + m4 + 4
+    o["loss"] = end + a4(2 * (2 + 2 * s))
+    return o
+
+
+@pytest.mark.parametrize("dec", ["sp", "rescal"])
+def test_forward_launch_alone_vs_oracle(built_lib, cuda_dev, dec):
+    """One forward launch by itself (rae_step_forward, no update) at the C3 / C5 shapes
+    (m=100, r=200, s=20, l=100: the compile-time-shape fast encoders): the exchange records of
+    batch 0 hold the relation probabilities P (RelationClassifier.py:35-36), SP's wC1 / wC2
+    (SelectionalPreferences.py:31-32) and per-example loss terms that sum to -cost * D
+    (OieModel.py:90) -- the forward half of SURVEY 8(b)'s entry points checked in isolation
+    against the float64 oracle's forward."""
+    import ctypes as C
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    m, r, s, l = 100, 200, 20, 100
+    data, gold = synthetic_dataset(300, 2000, 10, seed=7)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s,
+                             0.0, 0.0, "adagrad", "fwd", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=1)
+    ind.compile_function()
+    eng = ind.engine
+    n1, n2 = ind.draw_epoch_negatives()
+    eng.set_epoch_negatives(n1, n2)
+    p0 = _params(ind)
+    lib, st = eng.lib, C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.rae_build_index(eng.plan, 0, 1, st) == 0
+    assert lib.rae_set_cursor(eng.plan, 0, st) == 0
+    assert lib.rae_step_forward(eng.plan, 0, st) == 0
+    torch.cuda.synchronize()
+    eng.check()
+    assert eng.rec_floats > 0
+    rec = eng.exchange_buf.detach().cpu().double().numpy()[:l * eng.rec_floats].reshape(l, eng.rec_floats)
+    tr = data.split["train"]
+    rows = slice(0, l)
+    res = O.train_step_grads(dec, p0, tr.xFeats[rows], tr.args1[rows], tr.args2[rows],
+                             n1[:, rows], n2[:, rows], alpha=1.0)
+    o = _record_offsets(dec, m, r, s)
+    np.testing.assert_allclose(rec[:, o["P"]:o["P"] + m], res.P, rtol=1e-4, atol=1e-6)
+    if dec == "sp":
+        np.testing.assert_allclose(rec[:, o["V1"]:o["V1"] + r], res.P @ p0["C1"].T, rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(rec[:, o["V2"]:o["V2"] + r], res.P @ p0["C2"].T, rtol=1e-4, atol=1e-5)
+    D = 4 * l + 2 * l * s
+    np.testing.assert_allclose(rec[:, o["loss"]].sum(), -res.cost * D, rtol=2e-5)
+    # nothing was updated: the parameters are the ones the forward read
+    for k, v in _params(ind).items():
+        assert np.array_equal(v, p0[k]), k
