@@ -202,6 +202,31 @@ def cpu_baseline(data, cfg, l, budget_s, max_steps=200):
                 ms_per_step=1e3 * l / runs[best]["value"])
 
 
+def warm_up(eng, W, K, prebuilt, graphed):
+    """Capture every graph the warm-up and the timed steps replay (no capture inside the timed
+    region), then run the W warm-up steps.  A step with a collective the runtime cannot capture
+    (data-parallel exchange) falls back to eager launches; returns whether graphs are used.
+    (tests/test_dist.py::test_rccl_one_rank_captured_exchange exercises the fallback.)"""
+    import torch
+    try:
+        if graphed:
+            eng.capture_for(0, W)
+            eng.capture_for(W, K, last_advance=False)
+        eng.run(0, W, index=not prebuilt)
+    except RuntimeError as e:              # e.g. a collective the runtime cannot capture
+        if eng.exchange is None or not graphed:
+            raise
+        print(f"warning: graph capture of the data-parallel step failed ({e}); timing eager "
+              f"launches instead", file=sys.stderr)
+        graphed = False
+        eng.graph_chunk = 1
+        eng._graphs.clear()
+        eng.cursor_moved()
+        torch.cuda.synchronize()
+        eng.run(0, W, index=not prebuilt)
+    return graphed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,21 +301,7 @@ def main():
             eng.build_index(0, min(eng.index_window, W + K))
         exchange.rows(eng._dp_send, eng._dp_recv)
         torch.cuda.synchronize()
-    graphed = args.graph_chunk > 1
-    try:
-        if graphed:                        # capture every graph the warm-up and the timed
-            eng.capture_for(0, W)          # steps replay before running either (no capture
-            eng.capture_for(W, K, last_advance=False)   # inside the timed region)
-        eng.run(0, W, index=not prebuilt)
-    except RuntimeError as e:              # e.g. a collective the runtime cannot capture
-        if ws == 1 or not graphed:
-            raise
-        print(f"warning: graph capture of the data-parallel step failed ({e}); timing eager "
-              f"launches instead", file=sys.stderr)
-        graphed = False
-        eng.graph_chunk = 1
-        torch.cuda.synchronize()
-        eng.run(0, W, index=not prebuilt)
+    graphed = warm_up(eng, W, K, prebuilt, args.graph_chunk > 1)
     timed_graphs = eng.graph_sizes(W, K) if graphed else []
     torch.cuda.synchronize()
     rdist.barrier()

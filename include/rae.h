@@ -103,11 +103,13 @@ typedef struct rae_config {
                                 * replicas after every step)                                  */
 #define RAE_DPUPD_PARTITIONED 1 /* rank k updates the rows it owns (row % G == k) and pushes *
                                  * the next step's rows to the ranks that read them            */
-#define RAE_PRIV_AUTO 0       /* single-rank SP plans on the compile-time-shape forward (C3): a  *
-                               * row exactly one record of the global batch references is     *
-                               * updated by that example's forward workgroup, the update       *
-                               * launch keeps the shared rows and the dense tiles (same        *
-                               * arithmetic, bit-identical parameters)                         */
+#define RAE_PRIV_AUTO 0       /* every single-rank plan without a regulariser (lambda1 =       *
+                               * lambda2 = 0) and with 2 + 2s <= 64 record slots, any decoder: *
+                               * a row exactly one record of the global batch references is     *
+                               * left out of the update's row tasks and updated by per-example *
+                               * workgroups of the same update launch (task_private_rows; same  *
+                               * arithmetic as the one-record row task, bit-identical          *
+                               * parameters)                                                    */
 #define RAE_PRIV_OFF 1        /* every row updated by the update launch                        */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):

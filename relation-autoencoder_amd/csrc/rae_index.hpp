@@ -119,7 +119,10 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
         }
         return;
     }
-    const int H = index_partitions(nrec);
+    // partitioned data-parallel update: this rank keeps only the rows it owns (row % G == rank),
+    // ~nrec / G records, so it sizes its partitions from that share and hashes on row / G (row %
+    // H would leave whole partitions empty when gcd(G, H) > 1)
+    const int H = index_partitions(a.part ? (nrec + a.G - 1) / a.G : nrec);
     int base_i = 0, nh = 0, nl = 0, nv = 0;
     for (int h = 0; h < H; ++h) {
         if (tid == 0) sint[0] = 0;
@@ -147,7 +150,8 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
             }
             // partitioned data-parallel update: this rank's update visits only the rows it
             // owns (rae_dp.hpp)
-            if (row % H == h && (!a.part || row % a.G == a.rank)) {
+            const int hrow = a.part ? row / a.G : row;
+            if (hrow % H == h && (!a.part || row % a.G == a.rank)) {
                 const int sl = atomicAdd(&sint[0], 1);
                 if (sl < RAE_KCAP) keys[sl] = ((unsigned long long)(unsigned)row << 32) | rec;
             }

@@ -667,12 +667,18 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
 // 160 KB of decoder-matrix loads.  Issued before those loads, an LDS-DMA the pass cannot see
 // only ever makes its counted waits wait for more (vmcnt retires in issue order); the rows are
 // read after dma_visible_barrier (vmcnt(0) + barrier).
+// M0 is a reserved register the compiler cannot take as a clobber: the asm saves it into a
+// scratch SGPR and restores it behind the load (the instruction reads M0 at issue), so any M0
+// value the compiler keeps live across the block -- e.g. for its own global_load_lds -- is
+// unchanged.  tests/test_isa.py checks every LDS-DMA of the C3 forward in the code object.
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
 }
 __device__ __forceinline__ void dma_row16(const float* gsrc, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :: "v"(gsrc), "s"(lds) : "memory", "m0");
+    uint32_t saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved) : "v"(gsrc), "s"(lds) : "memory");
 }
 
 // record stores of the fast path

@@ -206,11 +206,21 @@ class TrainEngine:
         self._dp_caps = (ca, cw)
         self._graphs.clear()
 
+    def stale(self, accumulators: bool = True) -> bool:
+        """Partitioned update: whether this rank's replica misses rows its peers own that
+        changed since the last sync_replicas (parameters; with `accumulators`, their AdaGrad
+        state too).  Always False for the replicated update."""
+        if not self._dp:
+            return False
+        return "params" in self._stale or (accumulators and "acc" in self._stale)
+
     def sync_replicas(self, accumulators: bool = True):
         """Partitioned update: gather every A / Ab / W row (and AdaGrad accumulator) from its
         owner, so every rank holds the whole current model (labelling, checkpoints, tests).
-        No-op for the replicated update (replicas are identical after every step)."""
-        if not self._dp:
+        A COLLECTIVE when anything is stale: every rank must call it (ReconstructInducer.gather
+        before a rank-0-only save).  No-op when nothing is stale, and for the replicated update
+        (replicas are identical after every step)."""
+        if not self.stale(accumulators):
             return
         torch.cuda.synchronize(self.device)
         ts = [self._named["W"], self._named["A"], self._named["Ab"]]
@@ -237,21 +247,29 @@ class TrainEngine:
             pass
 
     def kernel_forms_in_use(self):
-        """The kernel forms the plan resolved for its shape (rae_plan_forms): sp_forward
-        fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep fused|kernel
-        (bf16 bilinear), dp_update, priv_rows forward|off (rows one record references
-        updated by the forward); None where a form does not apply."""
+        """The kernel forms the plan resolved for its shape (rae_plan_forms), named as
+        _lib.KERNEL_FORMS names them -- so the dict can be fed back as
+        TrainEngine(kernel_forms=...) / bench.py --kernel-form to pin the same run:
+        sp_forward fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep
+        auto|kernel (bf16 bilinear: the forward writes the R-gradient operands, or k_bil_prep
+        does), dp_update replicated|partitioned, priv_rows auto|off (rows one record of the
+        batch references updated per example, or by the row tasks).  Keys of forms that do not
+        apply to the decoder are left out."""
         out = _lib.RaeConfig()
         _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
         F = _lib.KERNEL_FORMS
         name = {key: {code: n for n, code in F[key].items()} for key in F}
         sp = self.cfg.decoder == 0
-        bf16 = not sp and bool(self.cfg.mfma_bf16)
-        return {"sp_forward": name["sp_forward"][out.sp_forward] if sp else None,
-                "bil_dp": name["bil_dp"][out.bil_dp] if not sp else None,
-                "bil_prep": ("kernel" if out.bil_prep == 1 else "fused") if bf16 else None,
-                "dp_update": name["dp_update"][out.dp_update],
-                "priv_rows": "per_example" if out.priv_rows == 0 else "off"}
+        res = {}
+        if sp:
+            res["sp_forward"] = name["sp_forward"][out.sp_forward]
+        else:
+            res["bil_dp"] = name["bil_dp"][out.bil_dp]
+            if self.cfg.mfma_bf16:
+                res["bil_prep"] = name["bil_prep"][out.bil_prep]
+        res["dp_update"] = name["dp_update"][out.dp_update]
+        res["priv_rows"] = name["priv_rows"][out.priv_rows]
+        return res
 
     def _moves(self):
         return int(self.lib.rae_cursor_moves(self.plan))
@@ -501,8 +519,10 @@ class TrainEngine:
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):
         """labels (int64) and probs (fp32) of rows [row0, row0+nrows) of a split with the
-        current W/Wb (RelationClassifier.py:39-48)."""
-        if "params" in self._stale:          # partitioned update: gather W from its owners
+        current W/Wb (RelationClassifier.py:39-48).  Partitioned update with stale rows: the
+        W rows are gathered from their owners first -- a collective, so every rank labels (or
+        ReconstructInducer.gather() ran on every rank before a single rank labels)."""
+        if self.stale(accumulators=False):   # partitioned update: gather W from its owners
             self.sync_replicas(accumulators=False)
         lab = torch.empty(nrows, dtype=torch.int64, device=self.device)
         pr = torch.empty((nrows, self.m), dtype=torch.float32, device=self.device) if probs else None

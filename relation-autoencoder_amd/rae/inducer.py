@@ -269,11 +269,21 @@ class ReconstructInducer:
             return 2
         raise Exception("Either 'train' split or 'train', 'valid' and 'test' splits should be defined")
 
+    def gather(self):
+        """Make this rank's replica whole (partitioned data-parallel update: every A / Ab / W
+        row and accumulator from its owner).  A collective -- call it on EVERY rank, e.g. before
+        a rank-0-only save_checkpoint or labelling pass; a no-op when nothing is stale and for
+        the replicated update."""
+        if self.engine is not None:
+            self.engine.sync_replicas(accumulators=True)
+
     def state_dict(self):
         """Parameters + AdaGrad accumulators + RNG state + epoch cursor (the reference's
         save() keeps only the parameters and loses the accumulators and the RNG position,
-        OieInduction.py:110-116, so a reloaded model cannot continue the same run)."""
-        if self.engine is not None:         # partitioned update: rows from their owners
+        OieInduction.py:110-116, so a reloaded model cannot continue the same run).
+        Partitioned data-parallel update: if rows are stale this gathers them (a collective:
+        all ranks must call it) -- call gather() on every rank first to save from one rank."""
+        if self.engine is not None and self.engine.stale(accumulators=True):
             self.engine.sync_replicas(accumulators=True)
         sd = {"params": {k: v.detach().cpu() for k, v in self.modelFunc.named_params().items()},
               "rng": self.rng.get_state(), "epoch": self.cur_epoch,

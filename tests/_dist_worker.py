@@ -17,6 +17,8 @@ MODE
              argument 3: the data-parallel update ("replicated" | "partitioned").
   oracle_part  the row-owner partitioned update's protocol on the float64 oracle.
   rows       rae.dist.Exchange.rows / sync_rows / max_int over gloo.
+  gpu_ckpt   partitioned update, gather() on every rank, then a rank-0-only checkpoint.
+  nccl1      one rank over RCCL: the captured exchange == no exchange, bitwise (run_nccl1).
 """
 import os
 import sys
@@ -229,11 +231,113 @@ def run_gpu_c3(out, steps=3, dp_update="replicated"):
         np.save(os.path.join(out, f"c3_{k}_{rk}.npy"), v.detach().cpu().numpy())
 
 
+def run_gpu_ckpt(out, decoder):
+    """Partitioned update, then a rank-0-only checkpoint: every rank calls gather() (the
+    collective), then rank 0 alone saves -- which must not start a collective -- and every
+    rank's replica equals the others'."""
+    from rae import dist as rdist
+    from rae.inducer import ReconstructInducer
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    data, gold = _dataset()
+    m, r, s, l = DP_SHAPE["m"], DP_SHAPE["r"], DP_SHAPE["s"], DP_SHAPE["l"]
+    ex = rdist.make_exchange(ws, rk)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), DP_SHAPE["epochs"], 0.1, l, r,
+                             m, s, 0.0, 0.0, "adagrad", "dp", decoder, False, True, False, 1.0,
+                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
+                             dp_update="partitioned")
+    ind.learn(verbose=False)
+    assert ind.engine.stale()
+    ind.gather()                                   # every rank
+    assert not ind.engine.stale()
+    if rk == 0:                                    # rank 0 alone: no collective may start here
+        ind.save_checkpoint(os.path.join(out, "ckpt_part.npz"))
+        lab, _ = ind.engine.label(ind.engine.split, 0, 64, probs=False)
+        np.save(os.path.join(out, "ckpt_labels.npy"), lab.cpu().numpy())
+    dist.barrier()
+    params = {k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()}
+    np.savez(os.path.join(out, f"ckpt_replica_{rk}.npz"), **params)
+
+
+def run_nccl1(out):
+    """One rank over RCCL (the "nccl" backend; one GPU forms a 1-rank communicator): the
+    data-parallel exchange as bench.py runs it at N > 1 -- an in-place all_gather_into_tensor
+    of the records between the forward and the update, captured into the step graphs -- must
+    leave parameters and costs bitwise equal to the same run with no exchange; the same with a
+    forced capture failure (bench.warm_up's eager fallback); and an all_to_all_single (the
+    partitioned update's row pull) captured into a graph and replayed delivers its blocks."""
+    import bench
+    from rae import dist as rdist
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    dev = torch.device("cuda", 0)
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+
+    class NoCapture(rdist.Exchange):
+        """An exchange the runtime 'cannot capture' (raises inside a graph capture)."""
+        def __call__(self, buf):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("collective not capturable (test)")
+            super().__call__(buf)
+
+    res = {}
+    W_, K_ = 6, 20
+    for name, exch in (("plain", None), ("rccl", rdist.Exchange(1, 0)),
+                       ("fallback", NoCapture(1, 0))):
+        data, gold = synthetic_dataset(6000, 3000, 16, seed=7)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 100, 200, 100, 20,
+                                 0.0, 0.0, "adagrad", "nccl1", "sp", False, True, False, 1.0,
+                                 device=dev, exchange=exch, graph_chunk=8)
+        ind.compile_function()
+        eng = ind.engine
+        eng.sample_epoch_negatives(ind.negativeSampler, "device")
+        rdist.warm_up(exch, eng.exchange_buf)
+        eng.build_index(0, W_ + K_)
+        graphed = bench.warm_up(eng, W_, K_, True, True)
+        eng.run(W_, K_, index=False, last_advance=False)
+        torch.cuda.synchronize()
+        eng.check()
+        res[name] = ({k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()},
+                     eng.costs[:W_ + K_].cpu().numpy(), graphed)
+        ind._drop_engine()
+    assert res["plain"][2] and res["rccl"][2] and not res["fallback"][2], \
+        [v[2] for v in res.values()]
+    for name in ("rccl", "fallback"):
+        assert np.array_equal(res[name][1], res["plain"][1]), name
+        for k, v in res["plain"][0].items():
+            assert np.array_equal(res[name][0][k], v), (name, k)
+    # the rows all-to-all, captured and replayed
+    ex = rdist.Exchange(1, 0)
+    send = torch.arange(4096, dtype=torch.float32, device=dev)
+    recv = torch.zeros_like(send)
+    ex.rows(send, recv)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.graph(g, stream=st):
+        send.add_(1.0)
+        ex.rows(send, recv)
+    torch.cuda.current_stream(dev).wait_stream(st)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(recv, torch.arange(4096, dtype=torch.float32, device=dev) + 3.0)
+    with open(os.path.join(out, "nccl1.ok"), "w") as fh:
+        fh.write(f"rccl {torch.cuda.nccl.version()}\n")
+
+
 def main():
     mode, out = sys.argv[1], sys.argv[2]
     dec = sys.argv[3] if len(sys.argv) > 3 else "sp"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("gloo")
+    if mode == "nccl1":                  # one rank over RCCL on the box's one GPU
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
     try:
         if mode == "exchange":
             run_exchange(out)
@@ -247,6 +351,10 @@ def main():
             run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated")
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated")
+        elif mode == "gpu_ckpt":
+            run_gpu_ckpt(out, dec)
+        elif mode == "nccl1":
+            run_nccl1(out)
         else:
             raise SystemExit(f"unknown mode {mode}")
         dist.barrier()

@@ -138,3 +138,31 @@ def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws):
         np.testing.assert_array_equal(gp[0][k], gr[k])
         err = np.abs(gp[0][k] - v)
         assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"
+
+
+@pytest.mark.gpu
+def test_partitioned_gather_then_rank0_checkpoint(built_lib, cuda_dev, tmp_path):
+    """under the partitioned update a checkpoint from rank 0 alone must not start a
+    collective.  Every rank calls ReconstructInducer.gather(); rank 0 then saves and labels by
+    itself; the checkpoint equals every rank's replica and the replicated run's parameters."""
+    _launch(["gpu_ckpt", str(tmp_path), "sp"], nproc=2, timeout=240)
+    _launch(["gpu", str(tmp_path), "sp", "replicated"], nproc=2)
+    ck = np.load(tmp_path / "ckpt_part.npz")
+    gr = np.load(tmp_path / "gpu_replicated_sp_0.npz")
+    for rk in range(2):
+        rep = np.load(tmp_path / f"ckpt_replica_{rk}.npz")
+        for k in rep.files:
+            np.testing.assert_array_equal(ck["param/" + k], rep[k])
+            np.testing.assert_array_equal(ck["param/" + k].astype(np.float64), gr[k])
+    assert np.load(tmp_path / "ckpt_labels.npy").shape == (64,)
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_captured_exchange(built_lib, cuda_dev, tmp_path):
+    """the RCCL ("nccl") branch of rae/dist.py on hardware -- one torchrun
+    rank (a 1-GPU box forms a 1-rank communicator): the in-place all-gather captured inside the
+    step graphs leaves the trained parameters and costs bitwise equal to the run without an
+    exchange; bench.warm_up's eager fallback (capture refused) too; a captured all_to_all_single
+    replays correctly."""
+    _launch(["nccl1", str(tmp_path)], nproc=1, timeout=300)
+    assert (tmp_path / "nccl1.ok").exists()

@@ -22,7 +22,52 @@ pytestmark = pytest.mark.gpu
 COST_RTOL = 2e-5
 
 
-def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234):
+LABEL_ROWS = 100_000      # rows of the trained split the relation assignments are checked on
+LABEL_MARGIN = 1e-5       # labels compared where the oracle's top-2 score margin exceeds this
+
+
+def _gpu_labels(eng, nrows=LABEL_ROWS):
+    """func['label_train'] on the device (rae_label, RelationClassifier.py:39-48) over the first
+    `nrows` rows of the trained split, with the parameters the steps left."""
+    lab, _ = eng.label(eng.split, 0, min(nrows, eng.split.N), probs=False)
+    return lab.cpu().numpy()
+
+
+def _scores(xs, W, Wb, n):
+    return np.asarray(xs.xFeats[:n].astype(np.float64) @ W) + Wb[None, :]
+
+
+def check_labels(got, xs, W, Wb, margin=LABEL_MARGIN, what="", W_gpu=None, Wb_gpu=None,
+                 min_decisive=0.9):
+    """Relation assignments (argmax S, S = X.W + Wb; RelationClassifier.py:39-48,
+    OieInduction.py:321-340) of the GPU equal the oracle's wherever the oracle's top-2 margin
+    exceeds `margin` -- and, given the GPU's trained W_gpu / Wb_gpu, also exceeds twice the row's
+    largest score difference between the two models (bf16 runs: the trajectories differ by the
+    operand rounding, so a label may only flip where the models' scores disagree by more than
+    the margin).  At least `min_decisive` of the rows must be checked.  Returns the share."""
+    n = got.shape[0]
+    S = _scores(xs, W, Wb, n)
+    top2 = np.partition(S, -2, axis=1)[:, -2:]
+    gap = top2[:, 1] - top2[:, 0]
+    need = np.full(n, margin)
+    if W_gpu is not None:
+        Sg = _scores(xs, W_gpu, Wb_gpu, n)
+        need = np.maximum(need, 2.0 * np.abs(Sg - S).max(axis=1))
+        # the kernel's argmax is the argmax of its own model's scores (fp32 sums: 1e-5 margin)
+        tg = np.partition(Sg, -2, axis=1)[:, -2:]
+        own = (tg[:, 1] - tg[:, 0]) > LABEL_MARGIN
+        assert np.all(got[own] == Sg[own].argmax(axis=1)), what
+    decisive = gap > need
+    want = S.argmax(axis=1)
+    bad = np.flatnonzero(decisive & (got != want))
+    agree = float((got == want).mean())
+    print(what, f"labels: {n} rows, {decisive.mean():.4f} decisive, agreement {agree:.5f}")
+    assert decisive.mean() >= min_decisive, (what, decisive.mean())
+    assert bad.size == 0, (what, bad[:10], got[bad[:10]], want[bad[:10]])
+    return float(decisive.mean())
+
+
+def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234, labels=False):
     import torch
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
@@ -48,6 +93,10 @@ def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234):
     got = eng.costs[:steps].cpu().numpy().astype(np.float64)
     params = {k: v.detach().cpu().double().numpy()
               for k, v in ind.modelFunc.named_params().items()}
+    if labels:
+        check_labels(_gpu_labels(eng), xs, tr.params["W"], tr.params["Wb"],
+                     what=f"N={N} m={m} r={r} s={s} l={l}", W_gpu=params["W"],
+                     Wb_gpu=params["Wb"])
     return np.array(want), got, tr.params, params, init
 
 
@@ -56,7 +105,7 @@ def test_c2_full_size(built_lib, cuda_dev):
     # neg 10, l = 100 (the compile-time C2 specialisation of the forward, scalar lanes: K is
     # not a multiple of 4)
     want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=100_000, d=2 ** 17, m=30, r=100,
-                                              s=10, l=100, ntrue=30, steps=6)
+                                              s=10, l=100, ntrue=30, steps=6, labels=True)
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
 
 
@@ -64,7 +113,7 @@ def test_c2_full_size(built_lib, cuda_dev):
 # bf16 MFMA operands (BASELINE config 5): the tolerance is derived per trajectory
 # --------------------------------------------------------------------------------------------
 def bf16_trajectories(cuda_dev, dec, N, d, m, r, s, l, ntrue, steps, seed_data=1234,
-                      graph_chunk=2):
+                      graph_chunk=2, labels=False):
     """The GPU bf16 path, the exact float64 oracle and the float64 oracle with the bf16
     operand rounding emulated (rae_oracle.bf16_round at the three R contractions), over the
     same first `steps` batches of an epoch from RandomState(2).  Returns dict of
@@ -97,6 +146,9 @@ def bf16_trajectories(cuda_dev, dec, N, d, m, r, s, l, ntrue, steps, seed_data=1
     eng.check()
     got = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
     out["gpu"] = (eng.costs[:steps].cpu().numpy().astype(np.float64), got)
+    if labels:
+        out["labels"] = _gpu_labels(eng)
+        out["xs"] = xs
     ind._drop_engine()
     return out, init
 
@@ -143,8 +195,15 @@ def test_c5_bench_size_bf16(built_lib, cuda_dev):
     float64 oracle with the derived bf16 tolerance (check_bf16) and the untouched-rows
     property."""
     out, init = bf16_trajectories(cuda_dev, "rescal", N=1_000_000, d=2 ** 17, m=100, r=200,
-                                  s=20, l=100, ntrue=100, steps=4)
+                                  s=20, l=100, ntrue=100, steps=4, labels=True)
     check_bf16(out, init, "c5 full size")
+    # relation assignments: against the bf16-emulating oracle (the same operand rounding) and
+    # against the exact float64 oracle, each where its top-2 margin is decisive
+    pg = out["gpu"][1]
+    for name, floor in (("emu", 0.9), ("exact", 0.5)):
+        p = out[name][1]
+        check_labels(out["labels"], out["xs"], p["W"], p["Wb"], what=f"c5 labels vs {name}",
+                     W_gpu=pg["W"], Wb_gpu=pg["Wb"], min_decisive=floor)
 
 
 def _run_oracle_only(N, d, m, r, s, l, ntrue, steps, seed_data=1234):
@@ -177,7 +236,7 @@ def _check(want_c, got_c, want_p, got_p, init, min_untouched=0.0):
 
 def test_headline_c3_full_size(built_lib, cuda_dev):
     want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=1_000_000, d=2 ** 17, m=100, r=200,
-                                              s=20, l=100, ntrue=100, steps=4)
+                                              s=20, l=100, ntrue=100, steps=4, labels=True)
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
 
 

@@ -546,11 +546,19 @@ def test_fast_paths_ragged_vs_oracle(built_lib, cuda_dev, dec):
     _assert_params_close(_params(ind), tr.params, "ragged-fast")
 
 
-@pytest.mark.parametrize("opt,values", [("adagrad", False), ("sgd", False), ("adagrad", True)])
-def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values):
+@pytest.mark.parametrize("opt,values,dec,bf16", [("adagrad", False, "sp", False),
+                                                 ("sgd", False, "sp", False),
+                                                 ("adagrad", True, "sp", False),
+                                                 ("adagrad", False, "rescal", False),
+                                                 ("adagrad", False, "rescal", True),
+                                                 ("adagrad", False, "rescal+sp", False),
+                                                 ("sgd", False, "rescal+sp", True)])
+def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values, dec, bf16):
     """Rows one record of the batch references, updated by per-example workgroups of the update
-    launch (rae.h RAE_PRIV_AUTO), train bit-identically to the update launch's row tasks doing
-    every row (priv_rows=off): same parameters, accumulators and costs."""
+    launch (rae.h RAE_PRIV_AUTO: every single-rank plan without a regulariser), train
+    bit-identically to the update launch's row tasks doing every row (priv_rows=off): same
+    parameters, accumulators and costs -- for SP and for the bilinear decoders, whose e2 row has
+    its own gradient vector (task_private_rows' XY branch: G2), fp32 and bf16 MFMA operands."""
     s = 20
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
@@ -561,10 +569,11 @@ def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values):
             x = data.split["train"].xFeats
             x.data = np.random.RandomState(5).uniform(0.5, 2.0, size=x.data.shape).astype(np.float32)
         ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 100, 200, 100, s,
-                                 0.0, 0.0, opt, "priv", "sp", False, True, False, 1.0,
-                                 device=cuda_dev, graph_chunk=2, kernel_forms={"priv_rows": form})
+                                 0.0, 0.0, opt, "priv", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, kernel_forms={"priv_rows": form},
+                                 mfma_bf16=bf16)
         ind.compile_function()
-        assert ind.engine.kernel_forms_in_use()["priv_rows"] == ("per_example" if form == "auto" else "off")
+        assert ind.engine.kernel_forms_in_use()["priv_rows"] == form
         ind.learn(verbose=False)
         acc = {}
         if ind.optimizer.accumulator is not None:

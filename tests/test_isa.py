@@ -1,0 +1,113 @@
+"""ISA checks on the gfx950 code object inside the built librae_hip.so (CPU only: the offload
+bundle is extracted and disassembled with the ROCm LLVM tools, no GPU needed).
+
+LDS-DMA (global_load_lds_*) takes its LDS destination from M0.  The C3 forward issues its A-row
+DMAs from inline asm (rae_sp.hpp dma_row16) so the compiler's wait-count pass does not see them;
+M0 is a reserved register, so the asm saves and restores it instead of clobbering it.  These
+tests pin, in the machine code that ships, that every LDS-DMA of the C3 forward has its own M0
+write earlier in the same basic block (no branch in between), separated from the DMA by a wait
+state, and that the asm hands M0 back (the value it saved) right after the DMA."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+LIB = os.path.join(ROOT, "relation-autoencoder_amd", "rae", "librae_hip.so")
+BUILD_LOG = os.path.join(ROOT, "relation-autoencoder_amd", "rae", "librae_hip.build.log")
+C3_FWD = "_Z9k_forwardILb1EN3rae7FixDimsILi100ELi200ELi20EEEEvNS0_8StepArgsE"
+
+
+def _tool(name):
+    p = os.path.join(LLVM, name)
+    if not os.path.exists(p):
+        pytest.skip(f"{p} not available")
+    return p
+
+
+@pytest.fixture(scope="module")
+def disasm(built_lib, tmp_path_factory):
+    d = tmp_path_factory.mktemp("isa")
+    fat, co = d / "fat.bin", d / "gfx950.co"
+    subprocess.run([_tool("llvm-objcopy"), "-O", "binary", "--only-section=.hip_fatbin", LIB,
+                    str(fat)], check=True)
+    subprocess.run([_tool("clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    out = subprocess.run([_tool("llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
+                         text=True).stdout
+    funcs, cur = {}, None
+    for line in out.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = funcs.setdefault(m.group(1), [])
+            continue
+        if cur is not None and line.startswith("\t"):
+            cur.append(line.split("//")[0].strip())
+    return funcs
+
+
+def _writes_m0(ins):
+    parts = ins.replace(",", " ").split()
+    return len(parts) > 1 and parts[0].startswith("s_") and parts[1] == "m0"
+
+
+def _ends_block(ins):
+    op = ins.split()[0] if ins else ""
+    return op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_endpgm"))
+
+
+def _lds_dma_sites(code):
+    return [i for i, ins in enumerate(code) if ins.startswith("global_load_lds")]
+
+
+def test_c3_forward_lds_dma_has_its_own_m0(disasm):
+    code = disasm.get(C3_FWD)
+    assert code, "the C3 forward kernel is not in the code object"
+    sites = _lds_dma_sites(code)
+    # one DMA per A row of the example: 1 + 2s = 41 rows over waves 4..7 (unrolled)
+    assert len(sites) >= 11, len(sites)
+    for i in sites:
+        j = i - 1
+        while j >= 0 and not _writes_m0(code[j]):
+            assert not _ends_block(code[j]), f"branch between M0 write and LDS-DMA at {i}"
+            j -= 1
+        assert j >= 0, f"no M0 write before the LDS-DMA at {i}"
+        assert code[j].startswith("s_mov_b32 m0,"), code[j]
+        # the M0 -> LDS-DMA hazard needs one wait state (the asm's s_nop; the compiler's own
+        # sites in the general fallback path put address arithmetic there)
+        assert i - j >= 2, "no wait state after the M0 write"
+
+
+def test_c3_forward_asm_restores_m0(disasm):
+    """dma_row16: s_mov_b32 sX, m0 ; s_mov_b32 m0, sY ; s_nop ; global_load_lds ; s_mov_b32 m0, sX"""
+    code = disasm[C3_FWD]
+    asm_sites = [i for i in _lds_dma_sites(code) if code[i - 1].startswith("s_nop")]
+    assert len(asm_sites) >= 11, len(asm_sites)     # (NR + 3) / 4 per wave, unrolled
+    for i in asm_sites:
+        save = code[i - 3].replace(",", " ").split()
+        restore = code[i + 1].replace(",", " ").split()
+        assert save[:1] == ["s_mov_b32"] and save[2] == "m0", code[i - 3]
+        assert restore[:2] == ["s_mov_b32", "m0"] and restore[2] == save[1], (code[i - 3], code[i + 1])
+
+
+def test_every_lds_dma_follows_an_m0_write(disasm):
+    """Every LDS-DMA in the library (compiler-emitted builtins included) has an M0 write earlier
+    in its function."""
+    n = 0
+    for name, code in disasm.items():
+        for i in _lds_dma_sites(code):
+            assert any(_writes_m0(c) for c in code[:i]), name
+            n += 1
+    assert n > 0
+
+
+def test_build_is_warning_free(built_lib):
+    """__graft_entry__.build() keeps the compiler's output next to the library."""
+    if not os.path.exists(BUILD_LOG):
+        pytest.skip("library built without a log (prebuilt)")
+    log = open(BUILD_LOG).read()
+    assert "warning:" not in log, log[:2000]
