@@ -75,6 +75,11 @@ __global__ __launch_bounds__(RAE_BT) void k_sp_fin(StepArgs a) {
     __shared__ float red[2 * RAE_NWAVE];
     sp_split_fin(a, blockIdx.x, red);
 }
+// SP wire record (data parallel): V1, V2, G1 of the whole global batch after the exchange
+__global__ __launch_bounds__(RAE_BT) void k_vrec(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
+    sp_vrec(a, blockIdx.x, red);
+}
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
 template <bool V4>
@@ -578,9 +583,15 @@ extern "C" int rae_version(void) { return RAE_VERSION; }
 __attribute__((used)) static const char g_build_id[] = "RAE_BUILD_ID:" RAE_BUILD_KIND RAE_BUILD_ID;
 extern "C" const char* rae_build_id(void) { return g_build_id + 13; }
 
+// the SP decoder exchanges wire records between ranks (rae_step.hpp): V1 / V2 / G1 are
+// recomputed after the all-gather instead of crossing xGMI
+static int wire_records(const rae_config& c) {
+    return c.decoder == RAE_DEC_SP && c.world_size > 1 ? 1 : 0;
+}
 extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
     if (!cfg) return -1;
-    return make_layout(cfg->decoder, cfg->relations, cfg->embed, cfg->neg_samples).rec;
+    return make_layout(cfg->decoder, cfg->relations, cfg->embed, cfg->neg_samples,
+                       wire_records(*cfg)).rec;
 }
 extern "C" int64_t rae_exchange_floats(const rae_config* cfg) {
     if (!cfg) return -1;
@@ -629,8 +640,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_INVALID, "AdaGrad accumulators required");
 
     {
-        const RecLayout lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples);
-        if ((int64_t)lay.rec * c.batch_size * c.world_size >= (1ll << 31))
+        const RecLayout lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples,
+                                          wire_records(c));
+        if ((int64_t)lay.rec * c.batch_size * c.world_size >= (1ll << 31) ||
+            (int64_t)3 * align4(c.embed) * c.batch_size * c.world_size >= (1ll << 31))
             return fail(RAE_E_INVALID, "exchange buffer exceeds 2^31 floats (global batch too large)");
     }
     rae_plan* p = new rae_plan();
@@ -674,7 +687,16 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.aW = buf->acc_W; a.aWb = buf->acc_Wb; a.aA = buf->acc_A; a.aAb = buf->acc_Ab;
     a.aC1 = buf->acc_C1; a.aC2 = buf->acc_C2; a.aR3 = buf->acc_R3;
     a.ex = buf->exchange;
-    a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples);
+    a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples, wire_records(c));
+    // the update's record vectors: in the records, or (wire record) the vector buffer
+    a.vb = a.ex;
+    a.vbs = a.lay.rec;
+    a.vG1 = a.lay.oG1; a.vV1 = a.lay.oV1; a.vV2 = a.lay.oV2; a.vG2 = a.lay.oG2;
+    if (a.lay.wire) {
+        const int r4 = align4(c.embed);
+        a.vbs = 3 * r4;
+        a.vV1 = 0; a.vV2 = r4; a.vG1 = 2 * r4; a.vG2 = 0;
+    }
     a.costs = buf->costs;
     p->v4 = (c.relations % 4 == 0) && (c.embed % 4 == 0);
     {
@@ -747,7 +769,15 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         a.dcap = cap;
         a.dstride = ((2 + NJd + cap) + 31) & ~31;     // whole 128-B lines per example
     }
-    const size_t o_desc = take(4ull * W_ * c.batch_size * a.dstride);
+    // private rows (rows one record of the global batch references, updated per example by the
+    // update launch): plans without a regulariser whose record slots fit one wave (NJ <= 64);
+    // the example's features from its descriptor (<= dcap, <= 32).  Several ranks: every rank's
+    // update takes the private rows it updates (replicated: all; partitioned: its own), so the
+    // descriptors cover the whole global batch
+    a.priv = (!a.reg_on && NJ <= 64 && c.priv_rows == RAE_PRIV_AUTO) ? 1 : 0;
+    a.dnx = (a.priv && c.world_size > 1) ? L : c.batch_size;
+    a.d0 = a.dnx == L ? c.rank * c.batch_size : 0;
+    const size_t o_desc = take(4ull * W_ * a.dnx * a.dstride);
     const size_t o_reg = take(16ull * (a.nregC + a.nregW + 1));
     const size_t o_gws = a.reg_on ? take(4ull * c.n_features * c.relations) : 0;
     // partitioned data-parallel update: list capacities are the worst cases of one rank's
@@ -786,15 +816,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                            (c.sp_forward == RAE_SPFWD_AUTO &&
                             (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
     const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
-    // private rows (rows one record of the batch references, updated per example): single-rank
-    // plans without a regulariser (a row then changes only through its records); the example's
-    // record slots in one wave (NJ <= 64), its features from the descriptor (<= dcap, <= 32)
-    a.priv = (c.world_size == 1 && !a.reg_on && NJ <= 64 && c.priv_rows == RAE_PRIV_AUTO) ? 1 : 0;
     a.privnf = a.priv ? (a.dcap < 32 ? a.dcap : 32) : 0;
-    const size_t o_pmask = a.priv ? take(16ull * W_ * c.batch_size) : 0;
+    const size_t o_pmask = a.priv ? take(16ull * W_ * L) : 0;
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
+    const size_t o_vb = a.lay.wire ? take(4ull * a.vbs * L) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
     if (e != hipSuccess) {
@@ -835,6 +862,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.dpc = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpc) : nullptr;
     a.dpmax = reinterpret_cast<int*>(p->ws + o_dpm);
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
+    if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -1072,6 +1100,8 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     a.step_offset = off;
     a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
+    if (a.lay.wire)           // the vectors the wire records left out, for the whole batch
+        RAE_LAUNCH(p, k_vrec, dim3(vrec_tasks(a.L, a.r)), bt, 0, st, a);
     if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
     else launch_update_q<1>(p, gu, bt, st, a);
     HIPCHK(hipGetLastError());

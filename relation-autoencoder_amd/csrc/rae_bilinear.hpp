@@ -126,7 +126,7 @@ __device__ void bil_encode_fast(const StepArgs& a, int64_t g, int bl, char* smem
     ExampleSmem S = carve_example_smem(smem, a.dec, m, r, s);
     const int bg = a.rank * a.l + bl;
     {
-        const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+        const int32_t* dsc = a.desc + ((g % a.index_window) * a.dnx + a.d0 + bl) * (int64_t)a.dstride;
         if (tid < a.dstride) {
             const int v = dsc[tid];
             if (tid == 0) S.sint[1] = v;                          // nf

@@ -287,13 +287,16 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
 // needs before its W-row gather in ONE coalesced read -- the feature count and CSR start,
 // the NJ entity ids (e1, e2, neg1[t], neg2[t]) and the first dcap feature ids -- instead of
 // the dependent indptr -> indices -> W-row chain (parameter independent, so built ahead).
+// With the update's private-row tasks on several ranks (dnx == L) every example of the global
+// batch gets one (each rank's update applies all examples' private rows, or its owned ones).
 template <int BT>
 __device__ void build_batch_desc(const StepArgs& a, int64_t g, int64_t slot) {
     const int NJ = 2 + 2 * a.s, DS = a.dstride;
-    int32_t* out = a.desc + slot * (int64_t)a.l * DS;
-    for (int idx = threadIdx.x; idx < a.l * DS; idx += BT) {
+    int32_t* out = a.desc + slot * (int64_t)a.dnx * DS;
+    const int first = a.dnx == a.L ? 0 : a.rank * a.l;
+    for (int idx = threadIdx.x; idx < a.dnx * DS; idx += BT) {
         const int bl = idx / DS, t = idx - bl * DS;
-        const int bg = a.rank * a.l + bl;
+        const int bg = first + bl;
         const int64_t ex = g * (int64_t)a.L + bg;
         const int64_t col = a.neg_mode ? ex : (int64_t)bg;
         const int p0 = a.indptr[ex];

@@ -134,7 +134,7 @@ template <class D>
 __device__ __forceinline__ void load_desc(const StepArgs& a, const D& Dm, int64_t g, int bl,
                                           ExampleSmem& S, bool ids = true) {
     const int NJ = 2 + 2 * Dm.s;                     // ids = false: S has no room for them
-    const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+    const int32_t* dsc = a.desc + ((g % a.index_window) * a.dnx + a.d0 + bl) * (int64_t)a.dstride;
     for (int t = threadIdx.x; t < a.dstride; t += RAE_FBT) {
         const int v = dsc[t];
         if (t == 0) S.sint[2] = v;
@@ -453,11 +453,17 @@ __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, Exa
     const float dl = S.scoef[0], dr = S.scoef[1];
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
         const float w1 = S.swC1[i], w2 = S.swC2[i];
-        rec[a.lay.oV1 + i] = w1;
-        rec[a.lay.oV2 + i] = w2;
         rec[a.lay.odw1 + i] = S.sdw1[i];
         rec[a.lay.odw2 + i] = S.sdw2[i];
-        rec[a.lay.oG1 + i] = dl * w1 + dr * w2;        // A[e1]: left and right both read it
+        if (!a.lay.wire) {                             // wire record: k_vrec rebuilds these
+            rec[a.lay.oV1 + i] = w1;
+            rec[a.lay.oV2 + i] = w2;
+            rec[a.lay.oG1 + i] = dl * w1 + dr * w2;    // A[e1]: left and right both read it
+        }
+    }
+    if (a.lay.wire && threadIdx.x == 0) {
+        rec[a.lay.oAux + 0] = dl;
+        rec[a.lay.oAux + 1] = dr;
     }
     for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
         const float* c = S.scoef + 3 * j;
@@ -770,7 +776,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     // the example's descriptor (rae_index.hpp build_batch_desc): feature count, CSR start,
     // entity ids and feature ids in one coalesced read
     {
-        const int32_t* dsc = a.desc + ((g % a.index_window) * a.l + bl) * (int64_t)a.dstride;
+        const int32_t* dsc = a.desc + ((g % a.index_window) * a.dnx + a.d0 + bl) * (int64_t)a.dstride;
         if (tid < a.dstride) {
             const int v = dsc[tid];
             if (tid == 0) S.sint[1] = v;                          // nf
@@ -1056,13 +1062,18 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
             reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
             rec_st(reinterpret_cast<float4*>(rec + (w == 0 ? a.lay.odw1 : a.lay.odw2)) + lane, v);
         }
-    } else if (w == 2) {                     // V1 = wC1, V2 = wC2
-        if (lv) {
+    } else if (w == 2) {                     // V1 = wC1, V2 = wC2 (wire record: k_vrec's)
+        if (lv && !a.lay.wire) {
             rec_st(reinterpret_cast<float4*>(rec + a.lay.oV1) + lane, wc1);
             rec_st(reinterpret_cast<float4*>(rec + a.lay.oV2) + lane, wc2);
         }
     } else if (w == 3) {                     // G1 = dl wC1 + dr wC2 (A[e1]'s gradient)
-        if (lv) {
+        if (a.lay.wire) {                    // wire record: (dl, dr) for k_vrec's G1
+            if (lane == 0) {
+                rec_st(rec + a.lay.oAux + 0, dl);
+                rec_st(rec + a.lay.oAux + 1, dr);
+            }
+        } else if (lv) {
             float4 gv;
             gv.x = dl * wc1.x + dr * wc2.x;
             gv.y = dl * wc1.y + dr * wc2.y;

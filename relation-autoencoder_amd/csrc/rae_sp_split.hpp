@@ -108,11 +108,64 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
     float o[4];
     sp_gemm_combine(acc, red, lane, w, o);
     if (w != 0) return;
-    const int oV = which ? a.lay.oV2 : a.lay.oV1;
+    // into the vectors the update reads (the record, or the wire record's vector buffer)
+    float* vb = const_cast<float*>(a.vb);
+    const int oV = which ? a.vV2 : a.vV1;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][i = li]
         const int bo = bt * 16 + 4 * g + reg;
-        if (bo < l && iv) a.ex[(int64_t)(a.rank * l + bo) * a.lay.rec + oV + i] = o[reg];
+        if (bo < l && iv) vb[(int64_t)(a.rank * l + bo) * a.vbs + oV + i] = o[reg];
+    }
+}
+
+// k_vrec (SP wire record, world_size > 1, after the exchange): V1 = P C1^T, V2 = P C2^T and
+// G1 = dl V1 + dr V2 for every example of the global batch into the vector buffer -- the
+// vectors the wire record leaves out.  Per output element the same K chunks in the same order
+// as k_sp_cp (one 4-wave workgroup per 16 x 16 tile of V1 and of V2 at once), so every rank
+// computes bit-identical vectors; task = (example tile, embedding tile).
+__host__ __device__ inline int vrec_tasks(int L, int r) { return ((L + 15) / 16) * ((r + 15) / 16); }
+__device__ void sp_vrec(const StepArgs& a, int task, float* red) {
+    const int L = a.L, m = a.m, r = a.r;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nit = (r + 15) / 16;
+    const int bt = task / nit, it = task - bt * nit;
+    const int li = lane & 15, g = lane >> 4;
+    const int b = bt * 16 + li, i = it * 16 + li;
+    const bool bv = b < L, iv = i < r, vec = (m & 3) == 0;
+    const float* Pr = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec + a.lay.oP;
+    float o[2][4];
+    const int nch = (m + 15) / 16;
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+        const float* Cr = (which ? a.C2 : a.C1) + (int64_t)(iv ? i : 0) * m;
+        rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
+            float4 x[RAE_SPG_U], y[RAE_SPG_U];
+#pragma unroll
+            for (int u = 0; u < RAE_SPG_U; ++u) {
+                const int k = (c0 + u * RAE_NWAVE) * 16 + 4 * g;
+                x[u] = load4_guard(Pr, k, m, bv, vec);
+                y[u] = load4_guard(Cr, k, m, iv, vec);
+            }
+#pragma unroll
+            for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+        }
+        sp_gemm_combine(acc, red, lane, w, o[which]);
+        __syncthreads();                                  // red reused by the second product
+    }
+    if (w != 0) return;
+    float* vb = const_cast<float*>(a.vb);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][i = li]
+        const int bo = bt * 16 + 4 * g + reg;
+        if (bo < L && iv) {
+            const float* rec = a.ex + (int64_t)bo * a.lay.rec;
+            const float dl = rec[a.lay.oAux + 0], dr = rec[a.lay.oAux + 1];
+            float* v = vb + (int64_t)bo * a.vbs;
+            v[a.vV1 + i] = o[0][reg];
+            v[a.vV2 + i] = o[1][reg];
+            v[a.vG1 + i] = dl * o[0][reg] + dr * o[1][reg];
+        }
     }
 }
 
@@ -174,9 +227,10 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 1);
     if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
     gather_rows_dma<V4>(a, Dm, S, NR, 1);
+    const float* vrow = a.vb + (int64_t)bg * a.vbs;          // k_sp_cp's V1, V2
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        S.swC1[i] = rec[a.lay.oV1 + i];
-        S.swC2[i] = rec[a.lay.oV2 + i];
+        S.swC1[i] = vrow[a.vV1 + i];
+        S.swC2[i] = vrow[a.vV2 + i];
     }
     __syncthreads();                                      // the A-row DMA has landed
     RAE_STAMP(a, 2);
@@ -193,7 +247,11 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
         rec[a.lay.odw1 + i] = S.sdw1[i];
         rec[a.lay.odw2 + i] = S.sdw2[i];
-        rec[a.lay.oG1 + i] = dl * S.swC1[i] + dr * S.swC2[i];   // A[e1]: left and right
+        if (!a.lay.wire) rec[a.lay.oG1 + i] = dl * S.swC1[i] + dr * S.swC2[i];   // A[e1]
+    }
+    if (a.lay.wire && threadIdx.x == 0) {                 // k_vrec rebuilds G1 from (dl, dr)
+        rec[a.lay.oAux + 0] = dl;
+        rec[a.lay.oAux + 1] = dr;
     }
     for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
         const float* c = S.scoef + 3 * j;

@@ -20,19 +20,38 @@ namespace rae {
 //            update kernel changes A); dw1/dw2 as SP for the hybrid.  Forward scratch:
 //            G1/G2 hold M a2 / M^T a1 until k_bil_fin, aux = (dOne, c_a1, c_a2) from
 //            k_bil_dec.
+//
+// Wire record (SP decoder, world_size > 1): what crosses xGMI in the all-gather.  V1, V2 and G1
+// are dropped -- every rank recomputes them for the whole global batch after the exchange
+// (k_vrec: V = P.C^T on fp32 MFMA, G1 = dl V1 + dr V2 from aux = (dl, dr)), which the update
+// reads from the vector buffer (StepArgs::vb) -- 692 instead of 1,288 floats per example at C3:
+//   P (m) | dS (m) | dw1 (r) | dw2 (r) | aux (4: dl, dr) | coef (2*NJ) | loss (1) | pad
 struct RecLayout {
     int oP, odS, oV1, oV2, odw1, odw2, oG1, ocoef, oloss, rec;
-    int oG2, oX, oY, oA1, oA2, oZ, oAux;   // bilinear decoders only (0 for SP)
+    int oG2, oX, oY, oA1, oA2, oZ, oAux;   // bilinear decoders (and oAux of the SP wire record)
+    int wire;                              // 1: SP wire record (no V1 / V2 / G1: -1)
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
 
-__host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s) {
+// wire: the SP decoder's data-parallel exchange record (ignored for the bilinear decoders)
+__host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s, int wire = 0) {
     RecLayout L{};
     const int NJ = 2 + 2 * s;
     const int m4 = align4(m), r4 = align4(r);
     L.oP = 0;
     L.odS = m4;
+    if (dec == 0 && wire) {
+        L.wire = 1;
+        L.oV1 = L.oV2 = L.oG1 = -1;
+        L.odw1 = 2 * m4;
+        L.odw2 = L.odw1 + r4;
+        L.oAux = L.odw2 + r4;
+        L.ocoef = L.oAux + 4;
+        L.oloss = L.ocoef + align4(2 * NJ);
+        L.rec = align4(L.oloss + 1);
+        return L;
+    }
     L.oV1 = 2 * m4;
     L.oV2 = L.oV1 + r4;
     L.odw1 = L.oV2 + r4;
@@ -78,6 +97,12 @@ struct StepArgs {
     // exchange records
     float* ex;
     RecLayout lay;
+    // the per-example gradient vectors the update reads for A rows: vec(e1) = G1, vec(e2) = G2
+    // (bilinear), vec(neg1) = V1, vec(neg2) = V2 -- example b's at vb + b * vbs + v* (floats).
+    // The records themselves (vb = ex, vbs = rec), or for the SP wire record the vector buffer
+    // k_vrec fills after the exchange (V1 | V2 | G1, 3 r4 floats per example of the batch)
+    const float* vb;
+    int vbs, vG1, vV1, vV2, vG2;
     // row index of the global batches (rae_index.hpp), one slot per batch % index_window
     int HA, HW, RA, RW, posbits;
     int64_t index_window;
@@ -94,6 +119,8 @@ struct StepArgs {
     // [nf, p0, entity ids (NJ), feature ids (<= dcap)], dstride ints each
     int32_t* desc;
     int dstride, dcap;
+    int dnx, d0;         // examples per descriptor slot (l; L when the update's private-row
+                         // tasks read every example's descriptor) and this rank's first one
     // batch addressing, outputs, scratch
     const int64_t* cursor;
     int64_t step_offset;

@@ -240,8 +240,8 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
     constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
     typedef typename VecT<V4>::T VT;
     const int nv = a.r / VW, s = a.s, NJ = 2 + 2 * s;
-    const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;   // SP: e2 has no A gradient (c = 0)
-    const RecBuf rb_(a.ex);
+    const int vo1 = XY ? a.vG2 : a.vV1;           // SP: e2 has no A gradient (c = 0)
+    const RecBuf rb_(a.vb);                       // the record vectors (rae_step.hpp vb)
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
         // a one-record row's record rides in its segment: no srec round trip
@@ -253,7 +253,7 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
         const float ga = er[1];
         if (lane >= n) cj = 0.f;
         gb += lane < n ? ga : 0.f;
-        const int vo = rb + (j == 0 ? a.lay.oG1 : (j == 1 ? vo1 : (j < 2 + s ? a.lay.oV1 : a.lay.oV2)));
+        const int vo = b * a.vbs + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
         // one round: U record vectors loaded (all issued before the first FMA), then summed
         // in record order -- the same order for every U, so the round width is free
         auto round = [&](auto Uc, int k0) {
@@ -512,7 +512,7 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
     const int b = t / (RAE_PRA + 1), sub = t - b * (RAE_PRA + 1);
     const int64_t slot = g % a.index_window;
     const int4 pm = reinterpret_cast<const int4*>(a.pmask)[slot * a.L + b];
-    const int32_t* dsc = a.desc + (slot * a.l + b) * (int64_t)a.dstride;      // G == 1: l == L
+    const int32_t* dsc = a.desc + (slot * a.dnx + b) * (int64_t)a.dstride;    // priv: dnx == L
     const float* rec = a.ex + (int64_t)b * a.lay.rec;
     if (sub < RAE_PRA) {                                      // A / Ab rows
         const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
@@ -520,9 +520,9 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
         const int sid = dsc[2 + (lane < NJ ? lane : 0)];
         const float2 cg = reinterpret_cast<const float2*>(rec + a.lay.ocoef)[lane < NJ ? lane : 0];
         // record vector of slot j: vec_0 = G1, vec_1 = G2 (bilinear) / V1, neg1 V1, neg2 V2
-        const int vo1 = XY ? a.lay.oG2 : a.lay.oV1;
-        const RecBuf rb_(a.ex);
-        const int rb0 = b * a.lay.rec;
+        const int vo1 = XY ? a.vG2 : a.vV1;
+        const RecBuf rb_(a.vb);
+        const int rb0 = b * a.vbs;
         // this wave's rows: marked bits wi, wi + 4 RAE_PRA, ... (wi = sub * 4 + w)
         uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
         for (int i = 0; i < sub * RAE_NWAVE + w; ++i) M &= M - 1;
@@ -540,7 +540,7 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
                 const int64_t e = __builtin_amdgcn_readlane(sid, j);
                 pv[k].load(a.A + e * r, nv, lane);
                 if (OPT == 0) av[k].load(a.aA + e * r, nv, lane); else av[k].zero();
-                const int vo = rb0 + (j == 0 ? a.lay.oG1 : (j == 1 ? vo1 : (j < 2 + s ? a.lay.oV1 : a.lay.oV2)));
+                const int vo = rb0 + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;

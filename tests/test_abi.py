@@ -38,7 +38,15 @@ def test_struct_layout_matches_header(built_lib):
     cfg.decoder = 0
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 100
     cfg.world_size = 8
-    assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 800
+    # data parallel, SP: the wire record (no V1 / V2 / G1; + aux (dl, dr) for k_vrec), 692
+    # floats instead of 1,288 per example at C3
+    wire = (2 * 100 + 2 * 200 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3
+    assert wire == 692
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == wire
+    assert built_lib.rae_exchange_floats(C.byref(cfg)) == wire * 800
+    cfg.decoder = 1     # the bilinear decoders exchange their whole record
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == \
+        ((3 * 100 + 10 * 200 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)
     assert built_lib.rae_version() >= 1
 
 

@@ -1,13 +1,19 @@
-"""Single-GPU cost model of the data-parallel update at world size G (no peers: the
-collectives are no-ops, the other ranks' records stay zero -- a timing probe only).
+"""Single-GPU cost model of the data-parallel step at world size G (no peers: the collectives
+are no-ops, the other ranks' records stay zero -- a timing probe only).
 
     python tools/probes/dp_update_model.py [--G 8] [--l 100] [--config c3]
+                                           [--link-gbs 76.8] [--links 7] [--eff 0.7] [--lat-us 10]
 
-Times, per step, rank 0's forward (l examples), the partitioned form's row pull kernels
-(rae_dp_pack + rae_dp_unpack, without the all-to-all) and the update over the global batch
-L = G*l -- replicated (every referenced row) vs partitioned (the rows rank 0 owns) -- with the
-kernels' own dispatch timestamps (rae_time_next), plus the bytes each all-to-all / all-gather
-would move.  DESIGN.md sec. 4 uses it for the per-step model of the 8-GPU run."""
+Times, per step, with the kernels' own dispatch timestamps (rae_time_next):
+  single       the G = 1 plan at the same l (the weak-scaling denominator): forward, update, and
+               the row index's per-batch cost over a window (bench.py counts it in the step);
+  replicated   rank 0 of a G-rank plan: forward (l examples), update over the global batch
+               L = G*l (with the SP wire record: k_vrec + k_update), row index of the global batch;
+  partitioned  the same with the row-owner partitioned update: + the row pull's pack / unpack.
+Bytes: the records all-gather and the rows all-to-all inbound per rank per step.  The
+projection puts each collective at  lat_us + inbound bytes / (links * link_gbs * eff)  on the
+step's critical path (no overlap with the kernels) and reports the weak-scaling efficiency
+t_single / t_G.  DESIGN.md sec. 4 holds the table of one run."""
 import argparse
 import ctypes as C
 import json
@@ -38,72 +44,120 @@ class NoPeers:
         pass
 
 
-def main():
+def measure(args, cfg, data, gold, G, mode):
     import torch
+    from rae.inducer import ReconstructInducer
+    dev = torch.device("cuda", 0)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
+                             cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
+                             True, False, 1.0, device=dev, world_size=G, rank=0,
+                             exchange=NoPeers(G) if G > 1 else None, graph_chunk=1,
+                             mfma_bf16=cfg.get("bf16", False), dp_update=mode)
+    ind.compile_function()
+    eng = ind.engine
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    n = min(args.iters, eng.nb, eng.index_window)
+    # the row index: per-batch cost over n batches (as the epoch loop builds a window)
+    st0 = torch.cuda.current_stream()
+    ie = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    eng.build_index(0, n)
+    torch.cuda.synchronize()
+    ie[0].record(st0)
+    eng.build_index(0, n)
+    ie[1].record(st0)
+    torch.cuda.synchronize()
+    index_us = ie[0].elapsed_time(ie[1]) * 1e3 / n
+    eng.set_cursor(0)
+    lib, plan = eng.lib, eng.plan
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def ev():
+        h = C.c_void_p()
+        assert lib.rae_event_create(C.byref(h)) == 0
+        return h
+    part = mode == "partitioned" and G > 1
+    t = {"forward": [], "update": []}
+    if part:
+        t.update(pack=[], unpack=[])
+    evs = []
+    for i in range(n):
+        e = {k: (ev(), ev()) for k in t}
+        if part:
+            assert lib.rae_time_next(plan, *e["pack"]) == 0
+            assert lib.rae_dp_pack(plan, i, st) == 0, lib.rae_last_error()
+            assert lib.rae_time_next(plan, *e["unpack"]) == 0
+            assert lib.rae_dp_unpack(plan, i, st) == 0, lib.rae_last_error()
+        assert lib.rae_time_next(plan, *e["forward"]) == 0
+        assert lib.rae_step_forward(plan, i, st) == 0
+        assert lib.rae_time_next(plan, *e["update"]) == 0
+        assert lib.rae_step_update(plan, i, st) == 0
+        evs.append(e)
+    torch.cuda.synchronize()
+    for e in evs:
+        for k in t:
+            v = C.c_float()
+            if lib.rae_event_elapsed_ms(e[k][0], e[k][1], C.byref(v)) == 0:
+                t[k].append(v.value * 1e3)
+    out = {k: float(np.median(v[3:])) for k, v in t.items() if v}
+    out["index_per_batch"] = index_us
+    out["record_floats"] = eng.rec_floats
+    if G > 1:
+        out["records_allgather_in_bytes"] = (G - 1) * args.l * eng.rec_floats * 4
+    if part:
+        ca, cw = eng._dp_caps
+        blk = int(lib.rae_dp_block_floats(C.byref(eng.cfg), ca, cw)) * 4
+        out["rows_alltoall_in_bytes"] = (G - 1) * blk
+        out["row_caps"] = [ca, cw]
+    out["kernel_forms"] = eng.kernel_forms_in_use()
+    ind._drop_engine()
+    return out
+
+
+def project(res, args):
+    bw = args.links * args.link_gbs * args.eff * 1e3          # bytes per us
+    coll = lambda b: args.lat_us + b / bw                      # noqa: E731
+    s = res["single"]
+    t1 = s["forward"] + s["update"] + s["index_per_batch"]
+    proj = {"single_step_us": t1,
+            "assumptions": {"link_gbs_per_direction": args.link_gbs, "links": args.links,
+                            "efficiency": args.eff, "collective_latency_us": args.lat_us,
+                            "inbound_GBs": bw / 1e3,
+                            "model": "step = index + [pack + A2A + unpack] + forward + AG + "
+                                     "update, every collective lat + bytes / inbound rate, "
+                                     "nothing overlapped"}}
+    for mode in ("replicated", "partitioned"):
+        r = res.get(mode)
+        if not r:
+            continue
+        tg = r["index_per_batch"] + r["forward"] + r["update"] + coll(r["records_allgather_in_bytes"])
+        if "pack" in r:
+            tg += r["pack"] + r["unpack"] + coll(r["rows_alltoall_in_bytes"])
+        proj[mode] = {"step_us": tg, "efficiency": t1 / tg}
+    return proj
+
+
+def main():
     import bench
     from rae.data import synthetic_dataset
-    from rae.inducer import ReconstructInducer
     ap = argparse.ArgumentParser()
     ap.add_argument("--G", type=int, default=8)
     ap.add_argument("--l", type=int, default=100)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--modes", default="replicated,partitioned")
+    ap.add_argument("--link-gbs", type=float, default=76.8,
+                    help="xGMI GB/s per link and direction (MI355X: 153.6 GB/s bidirectional)")
+    ap.add_argument("--links", type=int, default=7)
+    ap.add_argument("--eff", type=float, default=0.7, help="achievable fraction of the links")
+    ap.add_argument("--lat-us", type=float, default=10.0, help="per-collective latency")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
-    dev = torch.device("cuda", 0)
     data, gold = synthetic_dataset(cfg["N"], cfg["d"], cfg["ntrue"], seed=1234)
     res = {"G": args.G, "l": args.l, "config": args.config}
-    for mode in ("replicated", "partitioned"):
-        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
-                                 cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
-                                 True, False, 1.0, device=dev, world_size=args.G, rank=0,
-                                 exchange=NoPeers(args.G), graph_chunk=1,
-                                 mfma_bf16=cfg.get("bf16", False), dp_update=mode)
-        ind.compile_function()
-        eng = ind.engine
-        eng.sample_epoch_negatives(ind.negativeSampler, "device")
-        n = min(args.iters, eng.nb, eng.index_window)
-        eng.build_index(0, n)
-        eng.set_cursor(0)
-        lib, plan = eng.lib, eng.plan
-        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-
-        def ev():
-            h = C.c_void_p()
-            assert lib.rae_event_create(C.byref(h)) == 0
-            return h
-        t = {"forward": [], "pack": [], "unpack": [], "update": []}
-        evs = []
-        for i in range(n):
-            e = {k: (ev(), ev()) for k in t}
-            if mode == "partitioned":
-                assert lib.rae_time_next(plan, *e["pack"]) == 0
-                assert lib.rae_dp_pack(plan, i, st) == 0, lib.rae_last_error()
-                assert lib.rae_time_next(plan, *e["unpack"]) == 0
-                assert lib.rae_dp_unpack(plan, i, st) == 0, lib.rae_last_error()
-            assert lib.rae_time_next(plan, *e["forward"]) == 0
-            assert lib.rae_step_forward(plan, i, st) == 0
-            assert lib.rae_time_next(plan, *e["update"]) == 0
-            assert lib.rae_step_update(plan, i, st) == 0
-            evs.append(e)
-        torch.cuda.synchronize()
-        for e in evs:
-            for k in t:
-                if k in ("pack", "unpack") and mode != "partitioned":
-                    continue
-                v = C.c_float()
-                if lib.rae_event_elapsed_ms(e[k][0], e[k][1], C.byref(v)) == 0:
-                    t[k].append(v.value * 1e3)
-        out = {k: float(np.median(v[3:])) for k, v in t.items() if v}
-        rec = eng.rec_floats * 4
-        out["records_allgather_in_bytes"] = (args.G - 1) * args.l * rec
-        if mode == "partitioned":
-            ca, cw = eng._dp_caps
-            blk = int(lib.rae_dp_block_floats(C.byref(eng.cfg), ca, cw)) * 4
-            out["rows_alltoall_in_bytes"] = (args.G - 1) * blk
-            out["row_caps"] = [ca, cw]
-        res[mode] = out
-        ind._drop_engine()
+    res["single"] = measure(args, cfg, data, gold, 1, "replicated")
+    for mode in args.modes.split(","):
+        res[mode] = measure(args, cfg, data, gold, args.G, mode)
+    res["projection"] = project(res, args)
     print(json.dumps(res))
 
 
