@@ -749,6 +749,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_hdrA = take(16 * W_), o_hdrW = take(16 * W_);
     const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(16ull * W_ * a.RA);
     const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(16ull * W_ * a.RW);
+    const size_t o_srowA = a.HA > 1 ? take(4ull * W_ * a.RA) : 0;
+    const size_t o_srowW = a.HW > 1 ? take(4ull * W_ * a.RW) : 0;
     a.VCA = a.RA / (RAE_VHEAVY + 1) + 1;       // very heavy rows per batch are fewer than this
     a.VCW = a.RW / (RAE_VHEAVY + 1) + 1;
     const size_t o_vrowA = take(16ull * W_ * a.VCA), o_vrowW = take(16ull * W_ * a.VCW);
@@ -839,6 +841,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.urowA = reinterpret_cast<int32_t*>(p->ws + o_urowA);
 
     a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
+    a.srowA = a.HA > 1 ? reinterpret_cast<int32_t*>(p->ws + o_srowA) : nullptr;
+    a.srowW = a.HW > 1 ? reinterpret_cast<int32_t*>(p->ws + o_srowW) : nullptr;
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
     a.vrowA = reinterpret_cast<int32_t*>(p->ws + o_vrowA);
     a.vrowW = reinterpret_cast<int32_t*>(p->ws + o_vrowW);
@@ -866,7 +870,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP;
+    // keys, scan scratch, the batch's indptr, segment starts, partition sizes + cursors
+    p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP +
+                  8ull * (a.HA > a.HW ? a.HA : a.HW);
     p->smem_fwd = smem_ex;
     p->smem_spe = p->sp_split ? 4ull * example_smem_floats(0, c.relations, c.embed, 0) : 0;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;

@@ -108,6 +108,7 @@ struct StepArgs {
     int64_t index_window;
     int32_t *hdrA, *srecA, *urowA;      // urow*: interleaved (row, first position) pairs
     int32_t *hdrW, *srecW, *urowW;
+    int32_t *srowA, *srowW;             // build scratch: the rows of the records binned by partition
     int32_t *vrowA, *vrowW;             // very heavy rows' segments (VCA / VCW per slot)
     int VCA, VCW;
     // the update's dispatch table per slot (rae_index.hpp build_batch_tasks): every row task in

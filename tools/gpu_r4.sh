@@ -40,10 +40,16 @@ for st in "$@"; do
         || { echo $c bench failed; tail -20 $O/bench_$c.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/bench_$c.json')); print('$c', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: round(v, 2) for k, v in d['kernel_us'].items()})" ;;
     dpmodel:*)
-      l=${st#dpmodel:}
-      timeout -k 10 400 python3 -u tools/probes/dp_update_model.py --l $l > $O/dpmodel_$l.json 2> $O/dpmodel_$l.err \
-        || { echo dpmodel failed; tail -20 $O/dpmodel_$l.err; exit 1; }
-      cat $O/dpmodel_$l.json ;;
+      a=${st#dpmodel:}; l=${a%%:*}; f=""; tg=$l
+      if [ "$a" != "$l" ]; then f="--kernel-form ${a#*:}"; tg=${l}_$(echo ${a#*:} | tr -c 'a-zA-Z0-9' _); fi
+      timeout -k 10 400 python3 -u tools/probes/dp_update_model.py --l $l $f > $O/dpmodel_$tg.json 2> $O/dpmodel_$tg.err \
+        || { echo dpmodel failed; tail -20 $O/dpmodel_$tg.err; exit 1; }
+      python3 -c "
+import json; d=json.load(open('$O/dpmodel_$tg.json'))
+for k in ('single','replicated','partitioned'):
+    v=d.get(k)
+    if v: print(k, {x: (round(y,2) if isinstance(y,float) else y) for x,y in v.items() if x!='kernel_forms'})
+print('projection', {k: v for k, v in d['projection'].items() if k!='assumptions'})" ;;
     prof|prof:*)
       c=${st#prof}; c=${c#:}; c=${c:-c3}
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv \

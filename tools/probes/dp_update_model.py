@@ -52,21 +52,25 @@ def measure(args, cfg, data, gold, G, mode):
                              cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
                              True, False, 1.0, device=dev, world_size=G, rank=0,
                              exchange=NoPeers(G) if G > 1 else None, graph_chunk=1,
-                             mfma_bf16=cfg.get("bf16", False), dp_update=mode)
+                             mfma_bf16=cfg.get("bf16", False), dp_update=mode,
+                             kernel_forms=dict(kv.split("=", 1) for kv in args.kernel_form)
+                             if G > 1 else None)
     ind.compile_function()
     eng = ind.engine
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
-    n = min(args.iters, eng.nb, eng.index_window)
-    # the row index: per-batch cost over n batches (as the epoch loop builds a window)
+    # the row index: per-batch cost over a whole window (as the epoch loop builds it)
+    nw = min(eng.nb, eng.index_window)
     st0 = torch.cuda.current_stream()
     ie = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    eng.build_index(0, n)
+    eng.build_index(0, nw)
     torch.cuda.synchronize()
     ie[0].record(st0)
-    eng.build_index(0, n)
+    eng.build_index(0, nw)
     ie[1].record(st0)
     torch.cuda.synchronize()
-    index_us = ie[0].elapsed_time(ie[1]) * 1e3 / n
+    index_us = ie[0].elapsed_time(ie[1]) * 1e3 / nw
+    n = min(args.iters, eng.nb, eng.index_window)
+    eng.build_index(0, n)
     eng.set_cursor(0)
     lib, plan = eng.lib, eng.plan
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -145,6 +149,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default="replicated,partitioned")
+    ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
+                    help="kernel form of the G-rank plans (e.g. priv_rows=off)")
     ap.add_argument("--link-gbs", type=float, default=76.8,
                     help="xGMI GB/s per link and direction (MI355X: 153.6 GB/s bidirectional)")
     ap.add_argument("--links", type=int, default=7)
