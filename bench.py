@@ -414,10 +414,6 @@ def main():
                          "frac_min counts each byte this design moves once",
                 "frac_min": k["frac_min"], "timing": TIMING,
                 "traffic_source": None}
-        if traffic:
-            roof["traffic_source"] = (traffic.get("file", "") + ": " + traffic.get("source", ""))
-            roof["traffic_build_id"] = traffic.get("build_id")
-            roof["traffic_current"] = traffic.get("build_id") == build_id
     else:
         fl = step_flops(L, l, cfg["m"], cfg["r"], dec)
         pk = MFMA_BF16_PEAK_TFS if cfg.get("bf16") else MFMA_F32_PEAK_TFS
@@ -425,8 +421,15 @@ def main():
         roof = {"kernel": "step (forward phase + update phase)", "dominant_phase": dom,
                 "bound": "mfma", "achieved": ach,
                 "peak": pk, "unit": "TFLOP/s", "frac": ach / pk,
-                "traffic": None, "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
+                "traffic": kern[dom].get("traffic"), "traffic_of": dom + " phase, per step",
+                "flops_per_step": fl, "avg_step_kernel_us": fwd_us + upd_us,
                 "timing": TIMING}
+    if traffic:
+        # HBM (+ Infinity-Cache) bytes of the dominant kernel per launch from the committed PMC
+        # passes, and whether they profiled the library this run uses
+        roof["traffic_source"] = (traffic.get("file", "") + ": " + traffic.get("source", ""))
+        roof["traffic_build_id"] = traffic.get("build_id")
+        roof["traffic_current"] = traffic.get("build_id") == build_id
 
     # ---- labelling pass over the whole train split (func['label_train'] at full-split scale,
     # the encoder kernel K1 in inference mode): fixed weights, probs + labels
@@ -454,13 +457,22 @@ def main():
         nnz = int(split.indptr_np[Nl])
         lbytes = 4 * (Nl + 1) + 4 * nnz + 4 * nnz * cfg["m"] + 4 * Nl * cfg["m"] + 8 * Nl + 4 * cfg["m"]
         lach = lbytes / (lus * 1e-6) / 1e9
+        # compulsory HBM bytes: every input read once (indptr, feature ids, W once -- its rows
+        # are gathered again and again, from L2 / MALL), every output written once
+        cbytes = 4 * (Nl + 1) + 4 * nnz + 4 * cfg["d"] * cfg["m"] + 4 * Nl * cfg["m"] + 8 * Nl + \
+            4 * cfg["m"]
         label = {"kernel": "k_label (rae_label over the whole train split)", "rows": Nl,
                  "avg_launch_us": lus, "bytes_per_launch": lbytes, "achieved": lach,
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": lach / HBM_PEAK_GBS,
                  "rows_per_s": Nl / (lus * 1e-6),
                  "bytes": "per row 4 (indptr) + 4f (ids) + 4fm (W rows) + 4m (probs) + 8 (label); "
                           "no W-row reuse credited (SURVEY 8d) -- W (4dm bytes) is L2/MALL "
-                          "resident, so most of these bytes never reach HBM"}
+                          "resident, so most of these bytes never reach HBM",
+                 "compulsory_bytes": cbytes,
+                 "compulsory_frac": cbytes / (lus * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                 "compulsory": "each input read once from HBM (indptr, ids, W), probs + labels "
+                               "written once: the bytes that must cross HBM; 'frac' is the "
+                               "no-reuse gather rate (W rows mostly from MALL)"}
         lt = ((traffic or {}).get("per_kernel") or {}).get("rae::k_label")
         if lt:
             label["traffic"] = lt["traffic_bytes"]

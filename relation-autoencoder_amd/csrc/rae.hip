@@ -225,7 +225,7 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #define RAE_PRIV_ROWW 4       // private rows: row-task waves per example of the global batch
 #endif
 __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC, int L,
-                                               int priv) {
+                                               int priv, int privc) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
     const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
     int64_t rows = ((int64_t)TC * RAE_ROWPCT / 100 + RAE_NWAVE - 1) / RAE_NWAVE;
@@ -236,7 +236,7 @@ __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, in
         if (pr < rows) rows = pr;
     }
     if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
-    return (int64_t)nT + nP + NVC + rows + (priv ? (RAE_PRA + 1ll) * L : 0);
+    return (int64_t)nT + nP + NVC + rows + (priv ? (int64_t)priv_wgs_per_example(privc) * L : 0);
 }
 
 // LDS of one update workgroup: workgroup tasks' partials (a row: Q vectors per lane, or a tile:
@@ -263,8 +263,9 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
     int wgp = __builtin_amdgcn_readfirstlane(wg0);
     const int gw = wgp * RAE_NWAVE + w;
     const int64_t g = step_batch(a);
-    if (a.priv) {                 // private rows: (RAE_PRA + 1) L workgroups, dispatched
-        const int nX = (RAE_PRA + 1) * a.L;       // first (RAE_PRIV_LAST 0) or last
+    if (a.priv) {                 // private rows: (RAE_PRA + 1) L workgroups (1 per example when
+                                  // compact), dispatched first (RAE_PRIV_LAST 0) or last
+        const int nX = priv_wgs_per_example(a.privc) * a.L;
         const int x = RAE_PRIV_LAST ? wgp - (ngrid - nX) : wgp;
         if (x >= 0 && x < nX) {
             task_private_rows<OPT, V4, Q, BIL>(a, g, x, w, lane);
@@ -819,6 +820,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                             (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
     const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
     a.privnf = a.priv ? (a.dcap < 32 ? a.dcap : 32) : 0;
+    a.privc = (a.priv && a.part && c.world_size > 1) ? 1 : 0;
     const size_t o_pmask = a.priv ? take(16ull * W_ * L) : 0;
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
@@ -891,7 +893,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                    "workgroup (relations / embed / neg_samples too large)");
     }
     p->grid_fwd = c.batch_size;
-    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC, L, a.priv);
+    const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC, L, a.priv,
+                                   a.privc);
     if (gu >= (1ll << 31)) {
         (void)hipFree(p->ws);
         delete p;

@@ -164,6 +164,7 @@ struct StepArgs {
     // pmask per slot and example = (entity-slot bits j < 32, j >= 32, feature-position bits,
     // 0); the row index leaves these rows out of the update's dispatch table
     int priv, privnf;    // enabled; longest feature row whose rows may be private
+    int privc;           // one workgroup per example (partitioned plans: ~1/G of the rows)
     int32_t* pmask;
     unsigned long long* stamps;   // diagnostic build only (RAE_STAMPS): phase timestamps
 };

@@ -505,16 +505,24 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
 #ifndef RAE_PRA
 #define RAE_PRA 3            // workgroups per example for its A rows (+ 1 for its W rows)
 #endif
+// Partitioned data-parallel plans (StepArgs::privc): a rank owns ~1/G of each example's private
+// rows, so ONE workgroup per example takes them (waves 0-2 its A rows, wave 3 its W rows).
+__host__ __device__ inline int priv_wgs_per_example(int compact) { return compact ? 1 : RAE_PRA + 1; }
 template <int OPT, bool V4, int Q, bool XY>
 __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int PRM = Q == 1 ? RAE_PRMAX : RAE_PRMAX / 2;
-    const int b = t / (RAE_PRA + 1), sub = t - b * (RAE_PRA + 1);
+    const int pwe = priv_wgs_per_example(a.privc);
+    const int b = t / pwe, sub = t - b * pwe;
+    // this wave's share: A rows (marked bits wa0, wa0 + na, ...) or W rows (wf0, wf0 + nf, ...)
+    const bool doA = a.privc ? w < RAE_NWAVE - 1 : sub < RAE_PRA;
+    const int wa0 = a.privc ? w : sub * RAE_NWAVE + w, na = a.privc ? RAE_NWAVE - 1 : RAE_NWAVE * RAE_PRA;
+    const int wf0 = a.privc ? 0 : w, nfw = a.privc ? 1 : RAE_NWAVE;
     const int64_t slot = g % a.index_window;
     const int4 pm = reinterpret_cast<const int4*>(a.pmask)[slot * a.L + b];
     const int32_t* dsc = a.desc + (slot * a.dnx + b) * (int64_t)a.dstride;    // priv: dnx == L
     const float* rec = a.ex + (int64_t)b * a.lay.rec;
-    if (sub < RAE_PRA) {                                      // A / Ab rows
+    if (doA) {                                                // A / Ab rows
         const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
         // record j's entity id and coefficients (c_j, gamma_j) in lane j (NJ <= 64: plan)
         const int sid = dsc[2 + (lane < NJ ? lane : 0)];
@@ -523,9 +531,9 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
         const int vo1 = XY ? a.vG2 : a.vV1;
         const RecBuf rb_(a.vb);
         const int rb0 = b * a.vbs;
-        // this wave's rows: marked bits wi, wi + 4 RAE_PRA, ... (wi = sub * 4 + w)
+        // this wave's rows: marked bits wa0, wa0 + na, ...
         uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
-        for (int i = 0; i < sub * RAE_NWAVE + w; ++i) M &= M - 1;
+        for (int i = 0; i < wa0; ++i) M &= M - 1;
         while (M) {
             int jr[PRM];
             RowVec<V4, Q> pv[PRM], av[PRM], vv[PRM];
@@ -533,8 +541,7 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
 #pragma unroll
             for (int k = 0; k < PRM; ++k) {                   // a round: every load issued first
                 jr[k] = M ? __builtin_ctzll(M) : -1;
-#pragma unroll
-                for (int i = 0; i < RAE_NWAVE * RAE_PRA; ++i) M &= M - 1;
+                for (int i = 0; i < na; ++i) M &= M - 1;
                 if (jr[k] < 0) continue;
                 const int j = jr[k];
                 const int64_t e = __builtin_amdgcn_readlane(sid, j);
@@ -580,7 +587,7 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
             ds[q] = rv[a.lay.odS / VW + (c < nv ? c : 0)];
         }
         unsigned M = (unsigned)pm.z;
-        for (int i = 0; i < w; ++i) M &= M - 1;
+        for (int i = 0; i < wf0; ++i) M &= M - 1;
         (void)nf;
         while (M) {
             int fr[PRM];
@@ -589,8 +596,7 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
 #pragma unroll
             for (int k = 0; k < PRM; ++k) {
                 fr[k] = M ? __builtin_ctz(M) : -1;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) M &= M - 1;
+                for (int i = 0; i < nfw; ++i) M &= M - 1;
                 if (fr[k] < 0) continue;
                 const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
                 pv[k].load(a.W + f * m, nv, lane);

@@ -50,6 +50,13 @@ for k in ('single','replicated','partitioned'):
     v=d.get(k)
     if v: print(k, {x: (round(y,2) if isinstance(y,float) else y) for x,y in v.items() if x!='kernel_forms'})
 print('projection', {k: v for k, v in d['projection'].items() if k!='assumptions'})" ;;
+    dpprof:*)
+      a=${st#dpprof:}; l=${a%%:*}; f=""; tg=$l
+      if [ "$a" != "$l" ]; then f="--kernel-form ${a#*:}"; tg=${l}_$(echo ${a#*:} | tr -c 'a-zA-Z0-9' _); fi
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv \
+        -d $O/dpprof_$tg -o run -- python3 $R/tools/probes/dp_update_model.py --l $l $f \
+        > $O/dpprof_$tg.json 2> $O/dpprof_$tg.err) || { echo dpprof failed; tail -30 $O/dpprof_$tg.err; exit 1; }
+      cut -c1-150 $O/dpprof_$tg/run_kernel_stats.csv | head -20 ;;
     prof|prof:*)
       c=${st#prof}; c=${c#:}; c=${c:-c3}
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv \

@@ -5,8 +5,10 @@ share a pass on gfx950: MI355X_MICROARCH.md "rocprofv3 PMC slots").
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE  (gfx950 FETCH_SIZE tallies a wide coalesced read at
 half its bytes -- MI355X_MICROARCH.md "HBM"), averaged over the launches of each kernel; the
-step kernels are grouped as bench.py reports them: k_forward (SP: k_forward; bilinear: the
-five k_bil_* forward kernels per step) and k_update (k_update [+ k_dense_w]).
+step kernels are grouped as bench.py reports them, per STEP (a kernel launched twice a step,
+k_bil_mt, counts twice; steps = launches of the update kernel): k_forward (SP: k_forward or the
+split k_sp_* kernels; bilinear: the k_bil_* forward kernels) and k_update (k_vrec + k_update
+[+ k_dense_w]; bilinear k_bil_update ...).  k_label (the labelling pass) is per launch.
 FETCH_SIZE/WRITE_SIZE are in KB in rocprofv3's derived-counter output.
 """
 import argparse
@@ -34,7 +36,7 @@ def _group(name):
                                        "k_sp_fin"):
         return "k_forward", base
     if base in ("k_update", "k_update_bil", "k_bil_update", "k_bil_prep", "k_bil_rows", "k_dense_w",
-                "k_finalize_cost"):
+                "k_finalize_cost", "k_vrec"):
         return "k_update", base
     return None, base
 
@@ -74,12 +76,17 @@ def main():
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py "
                      f"--config {args.config} {' '.join(extra)}; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch",
            "per_kernel": per_kernel}
+    # per step: every kernel's total over the passes / the number of steps (the update kernel's
+    # launches; one per step)
+    steps = max((per_kernel[k]["launches"] for k in ("k_update", "k_update_bil", "k_bil_update")
+                 if k in per_kernel), default=0)
     groups = defaultdict(float)
     for base, v in per_kernel.items():
         g, _ = _group(base)
-        if g:
-            groups[g] += v["traffic_bytes"]
+        if g and steps:
+            groups[g] += v["traffic_bytes"] * v["launches"] / steps
     out.update(groups)
+    out["steps"] = steps
     # the library the passes profiled (bench.py compares it with the one it runs)
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
