@@ -88,6 +88,7 @@ typedef struct rae_config {
     int32_t bil_prep;         /* bf16 R-gradient operands: RAE_BILPREP_*                    */
     int32_t dp_update;        /* data-parallel update: RAE_DPUPD_*                          */
     int32_t priv_rows;        /* rows one record of the batch references: RAE_PRIV_*        */
+    int32_t dp_dense;         /* data-parallel SP: dense decoder-matrix gradients RAE_DPDENSE_* */
 } rae_config;
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
@@ -103,14 +104,23 @@ typedef struct rae_config {
                                 * replicas after every step)                                  */
 #define RAE_DPUPD_PARTITIONED 1 /* rank k updates the rows it owns (row % G == k) and pushes *
                                  * the next step's rows to the ranks that read them            */
-#define RAE_PRIV_AUTO 0       /* every single-rank plan without a regulariser (lambda1 =       *
-                               * lambda2 = 0) and with 2 + 2s <= 64 record slots, any decoder: *
-                               * a row exactly one record of the global batch references is     *
-                               * left out of the update's row tasks and updated by per-example *
-                               * workgroups of the same update launch (task_private_rows; same  *
-                               * arithmetic as the one-record row task, bit-identical          *
-                               * parameters)                                                    */
+#define RAE_PRIV_AUTO 0       /* every plan without a regulariser (lambda1 = lambda2 = 0) and   *
+                               * with 2 + 2s <= 64 record slots, any decoder: a row exactly one *
+                               * record of the global batch references is left out of the      *
+                               * update's row tasks and updated by per-example workgroups of the*
+                               * same update launch (task_private_rows; same arithmetic as the  *
+                               * one-record row task, bit-identical parameters).  Several ranks:*
+                               * every rank's update takes the private rows it updates (the     *
+                               * replicated update all of them, the partitioned one its own,   *
+                               * one workgroup per example)                                     */
 #define RAE_PRIV_OFF 1        /* every row updated by the update launch                        */
+#define RAE_DPDENSE_AUTO 0    /* partials when they are no larger than dw1 / dw2 in the records  *
+                               * (per-rank partial chunk <= 2 r + 8 floats: l >~ relations)      */
+#define RAE_DPDENSE_RECORDS 1 /* dw1 / dw2 of every example in the exchange records; the update *
+                               * reduces dC1 / dC2 / dWb over the global batch (K = L)           */
+#define RAE_DPDENSE_PARTIALS 2 /* each rank reduces its own l examples' dC1 / dC2 / dWb before   *
+                                * the exchange (k_dpart); the records carry the partial block,  *
+                                * the update sums the ranks' blocks in rank order               */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]

@@ -75,10 +75,15 @@ __global__ __launch_bounds__(RAE_BT) void k_sp_fin(StepArgs a) {
     __shared__ float red[2 * RAE_NWAVE];
     sp_split_fin(a, blockIdx.x, red);
 }
+// SP dense partials (data parallel): this rank's dC1 / dC2 / dWb into its records, before the exchange
+__global__ __launch_bounds__(RAE_BT) void k_dpart(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) rae_f4 sacc[RAE_BT];
+    dpart_tile(a, blockIdx.x, threadIdx.x >> 6, threadIdx.x & 63, sacc);
+}
 // SP wire record (data parallel): V1, V2, G1 of the whole global batch after the exchange
 __global__ __launch_bounds__(RAE_BT) void k_vrec(StepArgs a) {
-    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
-    sp_vrec(a, blockIdx.x, red);
+    const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
+    if (t < vrec_tasks(a.L, a.r)) sp_vrec(a, t, threadIdx.x & 63);
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
@@ -302,6 +307,20 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
 #endif
     if (wg < nT) {                                            // dense tiles
         RAE_FIRST(wg < nCt ? 0 : 2);
+        if (a.dpart) {                   // dense partials: the ranks' sums (wave 0), no K chain
+            if (w == 0) {
+                if (wg < nCt) {
+                    const int which = wg / (rt * mt), ti = wg - which * rt * mt;
+                    tile_from_partials<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r, false,
+                                            which * a.r * a.m, (ti / mt) * 16, (ti % mt) * 16, wg, lane);
+                } else {
+                    tile_from_partials<OPT>(a, a.Wb, a.aWb, 1, true, 2 * a.r * a.m, 0,
+                                            (wg - nCt) * 16, 0, lane);
+                }
+            }
+            RAE_WAVE_END();
+            return;
+        }
         if (wg < nCt) {
             const int which = wg / (rt * mt), ti = wg - which * rt * mt;
             wg_tile<OPT>(a, which ? a.C2 : a.C1, which ? a.aC2 : a.aC1, a.r,
@@ -585,14 +604,20 @@ __attribute__((used)) static const char g_build_id[] = "RAE_BUILD_ID:" RAE_BUILD
 extern "C" const char* rae_build_id(void) { return g_build_id + 13; }
 
 // the SP decoder exchanges wire records between ranks (rae_step.hpp): V1 / V2 / G1 are
-// recomputed after the all-gather instead of crossing xGMI
+// recomputed after the all-gather instead of crossing xGMI (1); with dense partials (2) the
+// records carry each rank's partial dC1 / dC2 / dWb block instead of every example's dw1 / dw2
 static int wire_records(const rae_config& c) {
-    return c.decoder == RAE_DEC_SP && c.world_size > 1 ? 1 : 0;
+    if (c.decoder != RAE_DEC_SP || c.world_size <= 1) return 0;
+    if (c.dp_dense == RAE_DPDENSE_RECORDS) return 1;
+    if (c.dp_dense == RAE_DPDENSE_PARTIALS) return 2;
+    const int pc = align4((dense_partial_floats(c.embed, c.relations) + c.batch_size - 1) /
+                          c.batch_size);
+    return pc <= 2 * align4(c.embed) + 8 ? 2 : 1;
 }
 extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
     if (!cfg) return -1;
     return make_layout(cfg->decoder, cfg->relations, cfg->embed, cfg->neg_samples,
-                       wire_records(*cfg)).rec;
+                       wire_records(*cfg), cfg->batch_size).rec;
 }
 extern "C" int64_t rae_exchange_floats(const rae_config* cfg) {
     if (!cfg) return -1;
@@ -614,9 +639,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.bil_dp < RAE_BILDP_AUTO || c.bil_dp > RAE_BILDP_MTILE ||
         c.bil_prep < RAE_BILPREP_AUTO || c.bil_prep > RAE_BILPREP_KERNEL ||
         c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED ||
-        c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_OFF)
+        c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_OFF ||
+        c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
-                                   "priv_rows)");
+                                   "priv_rows / dp_dense)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -642,7 +668,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     {
         const RecLayout lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples,
-                                          wire_records(c));
+                                          wire_records(c), c.batch_size);
         if ((int64_t)lay.rec * c.batch_size * c.world_size >= (1ll << 31) ||
             (int64_t)3 * align4(c.embed) * c.batch_size * c.world_size >= (1ll << 31))
             return fail(RAE_E_INVALID, "exchange buffer exceeds 2^31 floats (global batch too large)");
@@ -688,7 +714,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.aW = buf->acc_W; a.aWb = buf->acc_Wb; a.aA = buf->acc_A; a.aAb = buf->acc_Ab;
     a.aC1 = buf->acc_C1; a.aC2 = buf->acc_C2; a.aR3 = buf->acc_R3;
     a.ex = buf->exchange;
-    a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples, wire_records(c));
+    a.lay = make_layout(c.decoder, c.relations, c.embed, c.neg_samples, wire_records(c),
+                        c.batch_size);
     // the update's record vectors: in the records, or (wire record) the vector buffer
     a.vb = a.ex;
     a.vbs = a.lay.rec;
@@ -697,6 +724,15 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         const int r4 = align4(c.embed);
         a.vbs = 3 * r4;
         a.vV1 = 0; a.vV2 = r4; a.vG1 = 2 * r4; a.vG2 = 0;
+    }
+    // the forward's dw1 / dw2: in the records, or (dense partials) a rank-local buffer
+    a.dpart = a.lay.wire == 2 ? 1 : 0;
+    a.dwb = a.ex;
+    a.dws = a.lay.rec;
+    a.dw1o = a.lay.odw1; a.dw2o = a.lay.odw2;
+    if (a.dpart) {
+        a.dws = 2 * align4(c.embed);
+        a.dw1o = 0; a.dw2o = align4(c.embed);
     }
     a.costs = buf->costs;
     p->v4 = (c.relations % 4 == 0) && (c.embed % 4 == 0);
@@ -826,6 +862,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_vb = a.lay.wire ? take(4ull * a.vbs * L) : 0;
+    const size_t o_dwb = a.dpart ? take(4ull * a.dws * L) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
     hipError_t e = hipMalloc(&p->ws, off);
     if (e != hipSuccess) {
@@ -869,6 +906,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.dpmax = reinterpret_cast<int*>(p->ws + o_dpm);
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
     if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
+    if (a.dpart) a.dwb = reinterpret_cast<float*>(p->ws + o_dwb);
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -952,6 +990,8 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
                                                                     : RAE_BILPREP_KERNEL);
     out->dp_update = p->cfg.dp_update;
     out->priv_rows = p->args.priv ? RAE_PRIV_AUTO : RAE_PRIV_OFF;
+    out->dp_dense = p->args.lay.wire == 2 ? RAE_DPDENSE_PARTIALS
+                  : (p->args.lay.wire == 1 ? RAE_DPDENSE_RECORDS : 0);
     return RAE_OK;
 }
 
@@ -1053,7 +1093,11 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     a.cursor = cursor;
     a.step_offset = off;
     a.stamps = p->stamps_fwd;
-    if (a.dec == RAE_DEC_SP) launch_fwd_sp(p, a, st);
+    if (a.dec == RAE_DEC_SP) {
+        launch_fwd_sp(p, a, st);
+        if (a.dpart)          // this rank's dense partials into its records, before the exchange
+            RAE_LAUNCH(p, k_dpart, dim3(dpart_tasks(a.r, a.m)), dim3(RAE_BT), 0, st, a);
+    }
     else if (p->v4) launch_fwd_bil<true>(p, a, st);
     else launch_fwd_bil<false>(p, a, st);
     p->t_start = p->t_stop = nullptr;
@@ -1110,7 +1154,7 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
     if (a.lay.wire)           // the vectors the wire records left out, for the whole batch
-        RAE_LAUNCH(p, k_vrec, dim3(vrec_tasks(a.L, a.r)), bt, 0, st, a);
+        RAE_LAUNCH(p, k_vrec, dim3(ceil_div(vrec_tasks(a.L, a.r), RAE_NWAVE)), bt, 0, st, a);
     if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
     else launch_update_q<1>(p, gu, bt, st, a);
     HIPCHK(hipGetLastError());

@@ -444,7 +444,9 @@ __device__ __forceinline__ void softmax_backward(const StepArgs& a, const D& Dm,
 // write the common part of the exchange record
 template <class D>
 __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, ExampleSmem& S,
-                                             float* rec) {
+                                             int bg) {
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    float* dwr = a.dwb + (int64_t)bg * a.dws;
     const int m = Dm.m, r = Dm.r, NJ = 2 + 2 * Dm.s;
     for (int k = threadIdx.x; k < m; k += RAE_FBT) {
         rec[a.lay.oP + k] = S.sP[k];
@@ -453,8 +455,8 @@ __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, Exa
     const float dl = S.scoef[0], dr = S.scoef[1];
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
         const float w1 = S.swC1[i], w2 = S.swC2[i];
-        rec[a.lay.odw1 + i] = S.sdw1[i];
-        rec[a.lay.odw2 + i] = S.sdw2[i];
+        dwr[a.dw1o + i] = S.sdw1[i];
+        dwr[a.dw2o + i] = S.sdw2[i];
         if (!a.lay.wire) {                             // wire record: k_vrec rebuilds these
             rec[a.lay.oV1 + i] = w1;
             rec[a.lay.oV2 + i] = w2;
@@ -659,7 +661,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 9);
     softmax_backward(a, Dm, S);
     RAE_STAMP(a, 6);
-    write_record(a, Dm, S, a.ex + (int64_t)bg * a.lay.rec);
+    write_record(a, Dm, S, bg);
     RAE_STAMP(a, 7);
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
@@ -1060,7 +1062,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
                 vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lane]);
             }
             reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
-            rec_st(reinterpret_cast<float4*>(rec + (w == 0 ? a.lay.odw1 : a.lay.odw2)) + lane, v);
+            rec_st(reinterpret_cast<float4*>(a.dwb + (int64_t)bg * a.dws + (w == 0 ? a.dw1o : a.dw2o)) + lane, v);
         }
     } else if (w == 2) {                     // V1 = wC1, V2 = wC2 (wire record: k_vrec's)
         if (lv && !a.lay.wire) {

@@ -120,40 +120,53 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
 
 // k_vrec (SP wire record, world_size > 1, after the exchange): V1 = P C1^T, V2 = P C2^T and
 // G1 = dl V1 + dr V2 for every example of the global batch into the vector buffer -- the
-// vectors the wire record leaves out.  Per output element the same K chunks in the same order
-// as k_sp_cp (one 4-wave workgroup per 16 x 16 tile of V1 and of V2 at once), so every rank
-// computes bit-identical vectors; task = (example tile, embedding tile).
+// vectors the wire record leaves out.  One WAVE per 16 x 16 tile of V1 and V2 at once (no LDS, no
+// barrier: every operand load of the tile issued up front), yet per output element the same
+// arithmetic as k_sp_cp: chunk c (16 deep) goes to accumulator c % 4 (k_sp_cp's wave c % 4), the
+// four summed in order -- so the split forward's own vectors and every rank's are bit-identical.
+// task = (example tile, embedding tile).
+#define RAE_VR_KC 8
+static_assert(RAE_VR_KC % 4 == 0, "chunk u of a round feeds accumulator u % 4");
 __host__ __device__ inline int vrec_tasks(int L, int r) { return ((L + 15) / 16) * ((r + 15) / 16); }
-__device__ void sp_vrec(const StepArgs& a, int task, float* red) {
+__device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     const int L = a.L, m = a.m, r = a.r;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nit = (r + 15) / 16;
     const int bt = task / nit, it = task - bt * nit;
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, i = it * 16 + li;
     const bool bv = b < L, iv = i < r, vec = (m & 3) == 0;
     const float* Pr = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec + a.lay.oP;
-    float o[2][4];
+    const float* C1r = a.C1 + (int64_t)(iv ? i : 0) * m;
+    const float* C2r = a.C2 + (int64_t)(iv ? i : 0) * m;
     const int nch = (m + 15) / 16;
+    rae_f32x4 acc1[4], acc2[4];
 #pragma unroll
-    for (int which = 0; which < 2; ++which) {
-        const float* Cr = (which ? a.C2 : a.C1) + (int64_t)(iv ? i : 0) * m;
-        rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
-            float4 x[RAE_SPG_U], y[RAE_SPG_U];
+    for (int q = 0; q < 4; ++q) acc1[q] = acc2[q] = rae_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < nch; c0 += RAE_VR_KC) {          // one round at m <= 128
+        float4 x[RAE_VR_KC], y1[RAE_VR_KC], y2[RAE_VR_KC];
 #pragma unroll
-            for (int u = 0; u < RAE_SPG_U; ++u) {
-                const int k = (c0 + u * RAE_NWAVE) * 16 + 4 * g;
-                x[u] = load4_guard(Pr, k, m, bv, vec);
-                y[u] = load4_guard(Cr, k, m, iv, vec);
-            }
-#pragma unroll
-            for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+        for (int u = 0; u < RAE_VR_KC; ++u) {
+            const int k = (c0 + u) * 16 + 4 * g;           // >= m past the last chunk
+            const bool cv = c0 + u < nch;
+            x[u] = load4_guard(Pr, k, m, bv && cv, vec);
+            y1[u] = load4_guard(C1r, k, m, iv && cv, vec);
+            y2[u] = load4_guard(C2r, k, m, iv && cv, vec);
         }
-        sp_gemm_combine(acc, red, lane, w, o[which]);
-        __syncthreads();                                  // red reused by the second product
+#pragma unroll
+        for (int u = 0; u < RAE_VR_KC; ++u) {             // RAE_VR_KC % 4 == 0: chunk c0 + u
+            if (c0 + u < nch) {                            // -> accumulator u % 4
+                acc1[u & 3] = mfma4_f32(x[u], y1[u], acc1[u & 3]);
+                acc2[u & 3] = mfma4_f32(x[u], y2[u], acc2[u & 3]);
+            }
+        }
     }
-    if (w != 0) return;
+    // sp_gemm_combine's order: wave 0's accumulator, + wave 1's, + wave 2's, + wave 3's
+    rae_f32x4 o1 = acc1[0], o2 = acc2[0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+        o1 += acc1[q];
+        o2 += acc2[q];
+    }
     float* vb = const_cast<float*>(a.vb);
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][i = li]
@@ -162,9 +175,9 @@ __device__ void sp_vrec(const StepArgs& a, int task, float* red) {
             const float* rec = a.ex + (int64_t)bo * a.lay.rec;
             const float dl = rec[a.lay.oAux + 0], dr = rec[a.lay.oAux + 1];
             float* v = vb + (int64_t)bo * a.vbs;
-            v[a.vV1 + i] = o[0][reg];
-            v[a.vV2 + i] = o[1][reg];
-            v[a.vG1 + i] = dl * o[0][reg] + dr * o[1][reg];
+            v[a.vV1 + i] = o1[reg];
+            v[a.vV2 + i] = o2[reg];
+            v[a.vG1 + i] = dl * o1[reg] + dr * o2[reg];
         }
     }
 }
@@ -179,7 +192,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, k = kt * 16 + li;
     const bool bv = b < l, kv = k < m, vec = (r & 3) == 0;
-    const float* rec = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec;
+    const float* dwr = a.dwb + (int64_t)(a.rank * l + (bv ? b : 0)) * a.dws;
     const int kc = kv ? k : 0;
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int nci = (r + 15) / 16, nch = 2 * nci;
@@ -190,7 +203,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             const int c = c0 + u * RAE_NWAVE;
             const bool cv = c < nch;
             const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
-            const float* Dw = rec + (which ? a.lay.odw2 : a.lay.odw1);
+            const float* Dw = dwr + (which ? a.dw2o : a.dw1o);
             const float* Cm = which ? a.C2 : a.C1;
             x[u] = load4_guard(Dw, i, r, bv && cv, vec);
             y[u].x = (cv && kv && i < r) ? Cm[(int64_t)i * m + kc] : 0.f;
@@ -244,9 +257,10 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
     __syncthreads();
     RAE_STAMP(a, 5);
     const float dl = S.scoef[0], dr = S.scoef[1];
+    float* dwr = a.dwb + (int64_t)bg * a.dws;
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        rec[a.lay.odw1 + i] = S.sdw1[i];
-        rec[a.lay.odw2 + i] = S.sdw2[i];
+        dwr[a.dw1o + i] = S.sdw1[i];
+        dwr[a.dw2o + i] = S.sdw2[i];
         if (!a.lay.wire) rec[a.lay.oG1 + i] = dl * S.swC1[i] + dr * S.swC2[i];   // A[e1]
     }
     if (a.lay.wire && threadIdx.x == 0) {                 // k_vrec rebuilds G1 from (dl, dr)

@@ -26,30 +26,53 @@ namespace rae {
 // (k_vrec: V = P.C^T on fp32 MFMA, G1 = dl V1 + dr V2 from aux = (dl, dr)), which the update
 // reads from the vector buffer (StepArgs::vb) -- 692 instead of 1,288 floats per example at C3:
 //   P (m) | dS (m) | dw1 (r) | dw2 (r) | aux (4: dl, dr) | coef (2*NJ) | loss (1) | pad
+// With dense partials (wire 2, rae.h RAE_DPDENSE_PARTIALS) the rank reduces the decoder-matrix
+// gradients of its OWN l examples (k_dpart: dC1, dC2, dWb over K = l) and the records carry that
+// partial block -- pc floats each, rank k's element e in record k l + e / pc -- instead of dw1 /
+// dw2; the update sums the G partials in rank order (no K = L chain):
+//   P (m) | dS (m) | aux (4) | coef (2*NJ) | loss (1) | pad | partial chunk (pc)
 struct RecLayout {
     int oP, odS, oV1, oV2, odw1, odw2, oG1, ocoef, oloss, rec;
     int oG2, oX, oY, oA1, oA2, oZ, oAux;   // bilinear decoders (and oAux of the SP wire record)
-    int wire;                              // 1: SP wire record (no V1 / V2 / G1: -1)
+    int wire;                              // 1: SP wire record (no V1 / V2 / G1: -1); 2: + partials
+    int oPart, pc;                         // wire 2: the partial chunk (-1 / 0 otherwise)
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
 
 // wire: the SP decoder's data-parallel exchange record (ignored for the bilinear decoders)
-__host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s, int wire = 0) {
+// floats of one rank's dense partial block: dC1 (r, m) | dC2 (r, m) | dWb (m)
+__host__ __device__ inline int dense_partial_floats(int r, int m) { return 2 * r * m + m; }
+
+__host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s, int wire = 0,
+                                                 int l = 1) {
     RecLayout L{};
     const int NJ = 2 + 2 * s;
     const int m4 = align4(m), r4 = align4(r);
     L.oP = 0;
     L.odS = m4;
+    L.oPart = -1;
     if (dec == 0 && wire) {
-        L.wire = 1;
+        L.wire = wire;
         L.oV1 = L.oV2 = L.oG1 = -1;
-        L.odw1 = 2 * m4;
-        L.odw2 = L.odw1 + r4;
-        L.oAux = L.odw2 + r4;
+        int o = 2 * m4;
+        if (wire == 1) {
+            L.odw1 = o;
+            L.odw2 = o + r4;
+            o += 2 * r4;
+        } else {
+            L.odw1 = L.odw2 = -1;
+        }
+        L.oAux = o;
         L.ocoef = L.oAux + 4;
         L.oloss = L.ocoef + align4(2 * NJ);
-        L.rec = align4(L.oloss + 1);
+        o = align4(L.oloss + 1);
+        if (wire == 2) {
+            L.pc = align4((dense_partial_floats(r, m) + l - 1) / l);
+            L.oPart = o;
+            o += L.pc;
+        }
+        L.rec = o;
         return L;
     }
     L.oV1 = 2 * m4;
@@ -103,6 +126,12 @@ struct StepArgs {
     // k_vrec fills after the exchange (V1 | V2 | G1, 3 r4 floats per example of the batch)
     const float* vb;
     int vbs, vG1, vV1, vV2, vG2;
+    // where the forward leaves dCost/dwC1, dCost/dwC2 of example b (the dense C1 / C2 gradient
+    // operands): the record (dwb = ex), or -- dense partials -- a rank-local buffer that k_dpart
+    // reduces before the exchange
+    float* dwb;
+    int dws, dw1o, dw2o;
+    int dpart;           // dense partials (RecLayout wire 2)
     // row index of the global batches (rae_index.hpp), one slot per batch % index_window
     int HA, HW, RA, RW, posbits;
     int64_t index_window;

@@ -162,6 +162,96 @@ __device__ void wg_tile(const StepArgs& a, float* M, float* aM, int nrows, int o
     }
 }
 
+// ---- dense partials (data parallel, SP: RecLayout wire 2) ----------------------------------
+// Each rank reduces the decoder-matrix gradients of its OWN l examples before the exchange
+// (k_dpart: dC1, dC2 = sum_b dw_b P_b^T and dWb = sum_b dS_b, the same MFMA tile chain as wg_tile
+// with K = l split over four waves) into a partial block that rides in its records; the update
+// sums the G blocks in rank order -- K = l + G instead of a K = L chain per tile (which at
+// L = 8192 was the partitioned update's tail).  Element e of rank k's block: dpart_off.
+__device__ __forceinline__ int64_t dpart_off(const StepArgs& a, int k, int e) {
+    const int q = e / a.lay.pc;
+    return (int64_t)(k * a.l + q) * a.lay.rec + a.lay.oPart + (e - q * a.lay.pc);
+}
+__host__ __device__ inline int dpart_tasks(int r, int m) {
+    return 2 * ((r + 15) / 16) * ((m + 15) / 16) + (m + 15) / 16;
+}
+// tile t of this rank's partial block: C1 tiles, C2 tiles, Wb tiles (one workgroup each)
+__device__ void dpart_tile(const StepArgs& a, int t, int w, int lane, rae_f4* sacc) {
+    const int m = a.m, l = a.l, mt = (m + 15) / 16, nC = ((a.r + 15) / 16) * mt;
+    const int which = t < nC ? 0 : (t < 2 * nC ? 1 : 2);
+    const bool ones = which == 2;
+    const int ti = t - which * nC;
+    const int i0 = ones ? 0 : (ti / mt) * 16, k0 = (ones ? ti : ti % mt) * 16;
+    const int nrows = ones ? 1 : a.r;
+    const int li = lane & 15, lk = lane >> 4;
+    const int i = i0 + li, k = k0 + li;
+    const bool iv = i < nrows, kv = k < m;
+    const int q = ((l + 15) / 16) * 4;                   // examples per wave, multiple of 4
+    const int b0 = min(w * q, l), b1 = min(b0 + q, l);
+    const int64_t e0 = (int64_t)a.rank * l;
+    const float* Ar = a.dwb + (which == 1 ? a.dw2o : a.dw1o) + (iv ? i : 0);
+    const float* Br = a.ex + (ones ? a.lay.odS : a.lay.oP) + (kv ? k : 0);
+    rae_f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int bb = b0; bb < b1; bb += 4 * RAE_TU) {
+        float av[RAE_TU], bv[RAE_TU];
+#pragma unroll
+        for (int u = 0; u < RAE_TU; ++u) {               // every operand load before the chain
+            const int b = bb + 4 * u + lk;
+            const int64_t ex = e0 + (b < b1 ? b : b0);
+            av[u] = ones ? 1.f : Ar[ex * a.dws];
+            bv[u] = Br[ex * a.lay.rec];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < RAE_TU; ++u) {
+            const bool ok = bb + 4 * u + lk < b1;
+            const float x = (ok && iv && (!ones || li == 0)) ? av[u] : 0.f;
+            const float y = (ok && kv) ? bv[u] : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, acc, 0, 0, 0);
+        }
+    }
+    sacc[w * RAE_WAVE + lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    rae_f4 ts = sacc[lane];
+#pragma unroll
+    for (int ww = 1; ww < RAE_NWAVE; ++ww) ts += sacc[ww * RAE_WAVE + lane];
+    const int base = which * a.r * m;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {                  // D[row = 4 lk + reg][col = li]
+        const int row = i0 + lk * 4 + reg, col = k0 + li;
+        if (row < nrows && col < m && (!ones || row == i0))
+            a.ex[dpart_off(a, a.rank, base + (ones ? col : row * m + col))] = ts[reg];
+    }
+}
+
+// the update's tile task with dense partials: the G ranks' partial sums in rank order, then
+// the optimizer (one wave)
+template <int OPT>
+__device__ void tile_from_partials(const StepArgs& a, float* M, float* aM, int nrows, bool ones,
+                                   int base, int i0, int k0, int slot, int lane) {
+    float pw[4], pa[4];
+    tile_params<OPT>(a, M, aM, nrows, ones, i0, k0, lane, pw, pa);
+    const int li = lane & 15, lk = lane >> 4, col = k0 + li, m = a.m;
+    float v[4][8];
+    rae_f4 acc;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = i0 + lk * 4 + reg;
+        const bool ok = row < nrows && col < m && (!ones || row == i0);
+        const int e = ok ? base + (ones ? col : row * m + col) : 0;
+        float g = 0.f;
+        for (int k0g = 0; k0g < a.G; k0g += 8) {         // loads of 8 ranks in flight
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[reg][k] = k0g + k < a.G ? a.ex[dpart_off(a, k0g + k, e)] : 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) if (k0g + k < a.G) g += v[reg][k];
+        }
+        acc[reg] = g;
+    }
+    tile_apply<OPT>(a, M, aM, nrows, ones, i0, k0, slot, acc, pw, pa, lane);
+}
+
 // ---- the batch cost: -mean(all_scores) = -(sum_b loss_b) / (4L + 2Ls)  (OieModel.py:90)
 __device__ void task_cost(const StepArgs& a, int lane) {
     double loss = 0.0;

@@ -90,7 +90,7 @@ class RaeConfig(C.Structure):
         ("max_row_nnz", C.c_int32), ("neg_mode", C.c_int32), ("neg_stride", C.c_int64),
         ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
         ("sp_forward", C.c_int32), ("bil_dp", C.c_int32), ("bil_prep", C.c_int32),
-        ("dp_update", C.c_int32), ("priv_rows", C.c_int32),
+        ("dp_update", C.c_int32), ("priv_rows", C.c_int32), ("dp_dense", C.c_int32),
     ]
 
 
@@ -101,6 +101,7 @@ KERNEL_FORMS = {
     "bil_prep": {"auto": 0, "kernel": 1},
     "dp_update": {"replicated": 0, "partitioned": 1},
     "priv_rows": {"auto": 0, "off": 1},
+    "dp_dense": {"auto": 0, "records": 1, "partials": 2},
 }
 
 

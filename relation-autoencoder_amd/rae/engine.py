@@ -253,8 +253,9 @@ class TrainEngine:
         sp_forward fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep
         auto|kernel (bf16 bilinear: the forward writes the R-gradient operands, or k_bil_prep
         does), dp_update replicated|partitioned, priv_rows auto|off (rows one record of the
-        batch references updated per example, or by the row tasks).  Keys of forms that do not
-        apply to the decoder are left out."""
+        batch references updated per example, or by the row tasks), dp_dense records|partials
+        (data-parallel SP: dw1 / dw2 per example in the exchange, or each rank's reduced dense
+        gradients).  Keys of forms that do not apply to the plan are left out."""
         out = _lib.RaeConfig()
         _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
         F = _lib.KERNEL_FORMS
@@ -269,6 +270,8 @@ class TrainEngine:
                 res["bil_prep"] = name["bil_prep"][out.bil_prep]
         res["dp_update"] = name["dp_update"][out.dp_update]
         res["priv_rows"] = name["priv_rows"][out.priv_rows]
+        if sp and self.world_size > 1:
+            res["dp_dense"] = name["dp_dense"][out.dp_dense]
         return res
 
     def _moves(self):

@@ -183,7 +183,7 @@ def run_sync_rows(out):
     np.savez(os.path.join(out, f"rows_{rk}.npz"), recv=recv.numpy(), t2=t2.numpy(), t1=t1.numpy())
 
 
-def run_gpu(out, decoder, dp_update="replicated"):
+def run_gpu(out, decoder, dp_update="replicated", dense="auto"):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -195,8 +195,12 @@ def run_gpu(out, decoder, dp_update="replicated"):
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), DP_SHAPE["epochs"], 0.1, l, r,
                              m, s, 0.0, 0.0, "adagrad", "dp", decoder, False, True, False, 1.0,
                              device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
-                             dp_update=dp_update)
+                             dp_update=dp_update,
+                             kernel_forms={"dp_dense": dense} if decoder == "sp" else None)
     ind.learn(verbose=False)
+    if decoder == "sp":
+        want = "partials" if dense == "auto" else dense   # partials at DP_SHAPE (l = 15 > m)
+        assert ind.engine.kernel_forms_in_use()["dp_dense"] == want
     ind.engine.sync_replicas()
     params = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
     np.savez(os.path.join(out, f"gpu_{dp_update}_{decoder}_{rk}.npz"),
@@ -348,7 +352,8 @@ def main():
         elif mode == "rows":
             run_sync_rows(out)
         elif mode == "gpu":
-            run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated")
+            run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated",
+                    sys.argv[5] if len(sys.argv) > 5 else "auto")
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated")
         elif mode == "gpu_ckpt":

@@ -39,11 +39,23 @@ def test_struct_layout_matches_header(built_lib):
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == rec * 100
     cfg.world_size = 8
     # data parallel, SP: the wire record (no V1 / V2 / G1; + aux (dl, dr) for k_vrec), 692
-    # floats instead of 1,288 per example at C3
+    # floats instead of 1,288 per example at C3 with dw1 / dw2 in the records ...
+    cfg.dp_dense = 1
     wire = (2 * 100 + 2 * 200 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3
     assert wire == 692
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == wire
     assert built_lib.rae_exchange_floats(C.byref(cfg)) == wire * 800
+    # ... or with each rank's dense partial block (2 r m + m floats over its l records)
+    cfg.dp_dense = 2
+    pc = ((2 * 200 * 100 + 100 + 99) // 100 + 3) & ~3
+    part = ((2 * 100 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3) + pc
+    assert (pc, part) == (404, 696)
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == part
+    cfg.dp_dense = 0                 # auto: partials when no larger than dw1 / dw2 (l ~ m here)
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == part
+    cfg.batch_size = 40              # l << m: dw1 / dw2 are the smaller record
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == wire
+    cfg.batch_size = 100
     cfg.decoder = 1     # the bilinear decoders exchange their whole record
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == \
         ((3 * 100 + 10 * 200 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3)

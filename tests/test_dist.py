@@ -104,10 +104,17 @@ def test_partitioned_update_equals_global_batch(tmp_path, decoder, ws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal", 2), ("rescal+sp", 2), ("sp", 4),
-                                        ("sp", 8), ("rescal+sp", 8)])
-def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws):
-    _launch(["gpu", str(tmp_path), decoder], nproc=ws)
+@pytest.mark.parametrize("decoder,ws,dense", [("sp", 2, "auto"), ("rescal", 2, "auto"),
+                                              ("rescal+sp", 2, "auto"), ("sp", 4, "auto"),
+                                              ("sp", 8, "auto"), ("rescal+sp", 8, "auto"),
+                                              ("sp", 2, "records"), ("sp", 4, "records"),
+                                              ("sp", 8, "records")])
+def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws, dense):
+    """The HIP path on `ws` ranks sharing the GPU (replicated update) == the oracle at the
+    global batch, replicas bit-identical; SP both ways of moving the dense decoder-matrix
+    gradients (rae.h RAE_DPDENSE_*: auto = each rank's partials at this shape, or every
+    example's dw1 / dw2 in the records)."""
+    _launch(["gpu", str(tmp_path), decoder, "replicated", dense], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
     gs = [np.load(tmp_path / f"gpu_replicated_{decoder}_{k}.npz") for k in range(ws)]
     np.testing.assert_allclose(gs[0]["costs"], costs, rtol=2e-5, atol=2e-5)
@@ -119,14 +126,15 @@ def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder,ws", [("sp", 2), ("rescal+sp", 2), ("sp", 4), ("rescal", 4),
-                                        ("sp", 8)])
-def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws):
+@pytest.mark.parametrize("decoder,ws,dense", [("sp", 2, "auto"), ("rescal+sp", 2, "auto"),
+                                              ("sp", 4, "auto"), ("rescal", 4, "auto"),
+                                              ("sp", 8, "auto"), ("sp", 4, "records")])
+def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dense):
     """The HIP path with the row-owner partitioned update (k_build_dplists, k_dp_move, the
     owned-rows row index) on `ws` ranks sharing the GPU: == the oracle at the global batch,
     and bit-identical to the replicated update's parameters and costs."""
-    _launch(["gpu", str(tmp_path), decoder, "partitioned"], nproc=ws)
-    _launch(["gpu", str(tmp_path), decoder, "replicated"], nproc=ws)
+    _launch(["gpu", str(tmp_path), decoder, "partitioned", dense], nproc=ws)
+    _launch(["gpu", str(tmp_path), decoder, "replicated", dense], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
     gp = [np.load(tmp_path / f"gpu_partitioned_{decoder}_{k}.npz") for k in range(ws)]
     gr = np.load(tmp_path / f"gpu_replicated_{decoder}_0.npz")
