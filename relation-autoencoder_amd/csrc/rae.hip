@@ -58,18 +58,20 @@ __global__ __launch_bounds__(RAE_FBT) void k_sp_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     sp_split_enc<V4>(a, step_batch(a), blockIdx.x, smem);
 }
+template <bool VEC>
 __global__ __launch_bounds__(RAE_BT) void k_sp_cp(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
-    sp_split_cp(a, blockIdx.x, red);
+    sp_split_cp<VEC>(a, blockIdx.x, red);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_sp_dec(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     sp_split_dec<V4>(a, step_batch(a), blockIdx.x, smem);
 }
+template <bool VEC>
 __global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
-    sp_split_ctdw(a, blockIdx.x, red);
+    sp_split_ctdw<VEC>(a, blockIdx.x, red);
 }
 __global__ __launch_bounds__(RAE_BT) void k_sp_fin(StepArgs a) {
     __shared__ float red[2 * RAE_NWAVE];
@@ -81,9 +83,10 @@ __global__ __launch_bounds__(RAE_BT) void k_dpart(StepArgs a) {
     dpart_tile(a, blockIdx.x, threadIdx.x >> 6, threadIdx.x & 63, sacc);
 }
 // SP wire record (data parallel): V1, V2, G1 of the whole global batch after the exchange
+template <bool VEC>
 __global__ __launch_bounds__(RAE_BT) void k_vrec(StepArgs a) {
     const int t = blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6);
-    if (t < vrec_tasks(a.L, a.r)) sp_vrec(a, t, threadIdx.x & 63);
+    if (t < vrec_tasks(a.L, a.r)) sp_vrec<VEC>(a, t, threadIdx.x & 63);
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
@@ -229,19 +232,21 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_PRIV_ROWW
 #define RAE_PRIV_ROWW 4       // private rows: row-task waves per example of the global batch
 #endif
+// own: the share of the global batch's rows this rank updates (1 / G for the partitioned
+// data-parallel update: the row grid and the very heavy slots are sized from it)
 __host__ __device__ inline int64_t update_grid(int dec, int r, int m, int TC, int NVC, int L,
-                                               int priv, int privc) {
+                                               int priv, int privc, int own) {
     const int nT = n_ctiles(dec, r, m) + (m + 15) / 16;
     const int nP = (update_wave_free_tasks(dec, r, m) + RAE_NWAVE - 1) / RAE_NWAVE;
-    int64_t rows = ((int64_t)TC * RAE_ROWPCT / 100 + RAE_NWAVE - 1) / RAE_NWAVE;
+    int64_t rows = ((int64_t)TC * RAE_ROWPCT / 100 / own + RAE_NWAVE - 1) / RAE_NWAVE;
     // with the private rows (StepArgs::priv) taken per example by leading workgroups, the
     // dispatch table keeps ~5 % of the rows: a smaller row grid, grid-striding when a batch has more
     if (priv) {
-        const int64_t pr = ((int64_t)L * RAE_PRIV_ROWW + RAE_NWAVE - 1) / RAE_NWAVE;
+        const int64_t pr = ((int64_t)L * RAE_PRIV_ROWW / own + RAE_NWAVE - 1) / RAE_NWAVE;
         if (pr < rows) rows = pr;
     }
     if (RAE_UPD_WGCAP > 0 && rows > RAE_UPD_WGCAP) rows = RAE_UPD_WGCAP;
-    return (int64_t)nT + nP + NVC + rows + (priv ? (int64_t)priv_wgs_per_example(privc) * L : 0);
+    return (int64_t)nT + nP + NVC + rows + (priv ? (int64_t)priv_workgroups(privc, L) : 0);
 }
 
 // LDS of one update workgroup: workgroup tasks' partials (a row: Q vectors per lane, or a tile:
@@ -270,7 +275,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
     const int64_t g = step_batch(a);
     if (a.priv) {                 // private rows: (RAE_PRA + 1) L workgroups (1 per example when
                                   // compact), dispatched first (RAE_PRIV_LAST 0) or last
-        const int nX = priv_wgs_per_example(a.privc) * a.L;
+        const int nX = priv_workgroups(a.privc, a.L);
         const int x = RAE_PRIV_LAST ? wgp - (ngrid - nX) : wgp;
         if (x >= 0 && x < nX) {
             task_private_rows<OPT, V4, Q, BIL>(a, g, x, w, lane);
@@ -796,7 +801,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // wave tasks)
     a.TC = a.RA + a.RW;
     {
-        const int nvc = L / RAE_NVC_DIV > RAE_NVC_MIN ? L / RAE_NVC_DIV : RAE_NVC_MIN;
+        const int Lo = a.part ? (L + a.G - 1) / a.G : L;     // the rows this rank updates
+        const int nvc = Lo / RAE_NVC_DIV > RAE_NVC_MIN ? Lo / RAE_NVC_DIV : RAE_NVC_MIN;
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
     }
     const size_t o_thdr = take(16 * W_), o_task = take(16ull * W_ * a.TC);
@@ -932,7 +938,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     }
     p->grid_fwd = c.batch_size;
     const int64_t gu = update_grid(c.decoder, c.embed, c.relations, a.TC, a.NVC, L, a.priv,
-                                   a.privc);
+                                   a.privc, a.part ? a.G : 1);
     if (gu >= (1ll << 31)) {
         (void)hipFree(p->ws);
         delete p;
@@ -1036,10 +1042,12 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         const dim3 gcp(sp_cp_tasks(a.l, a.r)), gct(sp_ctdw_tasks(a.l, a.m));   // WG per tile
         if (p->v4) RAE_LAUNCH(p, k_sp_enc<true>, gr, bt, p->smem_spe, st, a);
         else RAE_LAUNCH(p, k_sp_enc<false>, gr, bt, p->smem_spe, st, a);
-        RAE_LAUNCH(p, k_sp_cp, gcp, dim3(RAE_BT), 0, st, a);
+        if (a.m % 4 == 0) RAE_LAUNCH(p, k_sp_cp<true>, gcp, dim3(RAE_BT), 0, st, a);
+        else RAE_LAUNCH(p, k_sp_cp<false>, gcp, dim3(RAE_BT), 0, st, a);
         if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gr, bt, p->smem_fwd, st, a);
         else RAE_LAUNCH(p, k_sp_dec<false>, gr, bt, p->smem_fwd, st, a);
-        RAE_LAUNCH(p, k_sp_ctdw, gct, dim3(RAE_BT), 0, st, a);
+        if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_BT), 0, st, a);
+        else RAE_LAUNCH(p, k_sp_ctdw<false>, gct, dim3(RAE_BT), 0, st, a);
         RAE_LAUNCH(p, k_sp_fin, gr, dim3(RAE_BT), 0, st, a);
         return;
     }
@@ -1154,7 +1162,11 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
     if (a.lay.wire)           // the vectors the wire records left out, for the whole batch
-        RAE_LAUNCH(p, k_vrec, dim3(ceil_div(vrec_tasks(a.L, a.r), RAE_NWAVE)), bt, 0, st, a);
+    {
+        const dim3 gv(ceil_div(vrec_tasks(a.L, a.r), RAE_NWAVE));
+        if (a.m % 4 == 0) RAE_LAUNCH(p, k_vrec<true>, gv, bt, 0, st, a);
+        else RAE_LAUNCH(p, k_vrec<false>, gv, bt, 0, st, a);
+    }
     if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
     else launch_update_q<1>(p, gu, bt, st, a);
     HIPCHK(hipGetLastError());

@@ -146,11 +146,13 @@ __device__ void dp_move(const StepArgs& a, int64_t t, int lane) {
     const int64_t slot = step_batch(a) % a.index_window;
     const int tab = i0 >= a.capA ? 1 : 0;
     const int i = tab ? i0 - a.capA : i0;
-    const int n = *dpl_count(a, slot, PACK ? 0 : 1, p, tab);
     const int cap = tab ? a.capW : a.capA;
+    // the list length and the entry load together (one round trip; the list's storage holds
+    // LA / LW >= cap entries, so entry i < cap is always in bounds -- used only when i < n)
+    const int n = *dpl_count(a, slot, PACK ? 0 : 1, p, tab);
+    const int row = dpl_list(a, slot, PACK ? 0 : 1, p, tab)[i < cap ? i : 0];
     if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);   // the host sizes cap >= every n
     if (i >= n || i >= cap) return;
-    const int row = dpl_list(a, slot, PACK ? 0 : 1, p, tab)[i];
     const int w = tab ? a.m : a.r, w4 = align4(w);
     float* blk = (PACK ? a.dsend : a.drecv) + (int64_t)p * a.dblk;
     float* buf = tab ? blk + (int64_t)a.capA * align4(a.r) + align4(a.capA) + (int64_t)i * w4

@@ -46,13 +46,24 @@ __device__ __forceinline__ rae_f32x4 mfma4_f32(const float4 x, const float4 y, r
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, y.w, acc, 0, 0, 0);
     return acc;
 }
-__device__ __forceinline__ float4 load4_guard(const float* p, int k, int n, bool ok, bool vec) {
-    if (vec) return (ok && k < n) ? *reinterpret_cast<const float4*>(p + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+// branch-free: the load always issues (clamped to element 0, always valid) and the value is
+// selected after -- a guarded load compiles to an exec-masked branch per load, and the branches
+// serialised every operand load of the GEMM tiles behind its own wait
+template <bool VEC>
+__device__ __forceinline__ float4 load4_guard(const float* p, int k, int n, bool ok) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (VEC) {                                       // n % 4 == 0: k < n covers k + 3
+        const bool in = ok && k < n;
+        const float4 v = *reinterpret_cast<const float4*>(p + (in ? k : 0));
+        return in ? v : z4;
+    }
     float4 v;
-    v.x = (ok && k < n) ? p[k] : 0.f;
-    v.y = (ok && k + 1 < n) ? p[k + 1] : 0.f;
-    v.z = (ok && k + 2 < n) ? p[k + 2] : 0.f;
-    v.w = (ok && k + 3 < n) ? p[k + 3] : 0.f;
+    const float x0 = p[(ok && k < n) ? k : 0], x1 = p[(ok && k + 1 < n) ? k + 1 : 0];
+    const float x2 = p[(ok && k + 2 < n) ? k + 2 : 0], x3 = p[(ok && k + 3 < n) ? k + 3 : 0];
+    v.x = (ok && k < n) ? x0 : 0.f;
+    v.y = (ok && k + 1 < n) ? x1 : 0.f;
+    v.z = (ok && k + 2 < n) ? x2 : 0.f;
+    v.w = (ok && k + 3 < n) ? x3 : 0.f;
     return v;
 }
 
@@ -81,6 +92,7 @@ __device__ __forceinline__ void sp_gemm_combine(rae_f32x4 acc, float* red, int l
 
 // k_sp_cp: tile (example, i) of V1 or V2.  A = P (rows b, K = k), B = C^T (K = k, columns i):
 // both K-contiguous, one float4 per lane per 16-deep chunk.
+template <bool VEC>
 __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
     const int l = a.l, m = a.m, r = a.r;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -89,7 +101,7 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
     const int bt = t2 / nit, it = t2 - bt * nit;
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, i = it * 16 + li;
-    const bool bv = b < l, iv = i < r, vec = (m & 3) == 0;
+    const bool bv = b < l, iv = i < r;
     const float* Pr = a.ex + (int64_t)(a.rank * l + (bv ? b : 0)) * a.lay.rec + a.lay.oP;
     const float* Cr = (which ? a.C2 : a.C1) + (int64_t)(iv ? i : 0) * m;
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -99,8 +111,8 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
 #pragma unroll
         for (int u = 0; u < RAE_SPG_U; ++u) {
             const int k = (c0 + u * RAE_NWAVE) * 16 + 4 * g;     // >= m past the last chunk
-            x[u] = load4_guard(Pr, k, m, bv, vec);
-            y[u] = load4_guard(Cr, k, m, iv, vec);
+            x[u] = load4_guard<VEC>(Pr, k, m, bv);
+            y[u] = load4_guard<VEC>(Cr, k, m, iv);
         }
 #pragma unroll
         for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
@@ -128,13 +140,14 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
 #define RAE_VR_KC 8
 static_assert(RAE_VR_KC % 4 == 0, "chunk u of a round feeds accumulator u % 4");
 __host__ __device__ inline int vrec_tasks(int L, int r) { return ((L + 15) / 16) * ((r + 15) / 16); }
+template <bool VEC>
 __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     const int L = a.L, m = a.m, r = a.r;
     const int nit = (r + 15) / 16;
     const int bt = task / nit, it = task - bt * nit;
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, i = it * 16 + li;
-    const bool bv = b < L, iv = i < r, vec = (m & 3) == 0;
+    const bool bv = b < L, iv = i < r;
     const float* Pr = a.ex + (int64_t)(bv ? b : 0) * a.lay.rec + a.lay.oP;
     const float* C1r = a.C1 + (int64_t)(iv ? i : 0) * m;
     const float* C2r = a.C2 + (int64_t)(iv ? i : 0) * m;
@@ -148,9 +161,9 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
         for (int u = 0; u < RAE_VR_KC; ++u) {
             const int k = (c0 + u) * 16 + 4 * g;           // >= m past the last chunk
             const bool cv = c0 + u < nch;
-            x[u] = load4_guard(Pr, k, m, bv && cv, vec);
-            y1[u] = load4_guard(C1r, k, m, iv && cv, vec);
-            y2[u] = load4_guard(C2r, k, m, iv && cv, vec);
+            x[u] = load4_guard<VEC>(Pr, k, m, bv && cv);
+            y1[u] = load4_guard<VEC>(C1r, k, m, iv && cv);
+            y2[u] = load4_guard<VEC>(C2r, k, m, iv && cv);
         }
 #pragma unroll
         for (int u = 0; u < RAE_VR_KC; ++u) {             // RAE_VR_KC % 4 == 0: chunk c0 + u
@@ -184,6 +197,7 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
 
 // k_sp_ctdw: tile (example, k) of dP.  A = dw (rows b, K = i: one float4 per lane per chunk),
 // B = C (K = i rows, columns k: four strided scalars per lane); K runs over C1's then C2's i.
+template <bool VEC>
 __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int l = a.l, m = a.m, r = a.r;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -191,7 +205,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int bt = task / nkt, kt = task - bt * nkt;
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, k = kt * 16 + li;
-    const bool bv = b < l, kv = k < m, vec = (r & 3) == 0;
+    const bool bv = b < l, kv = k < m;
     const float* dwr = a.dwb + (int64_t)(a.rank * l + (bv ? b : 0)) * a.dws;
     const int kc = kv ? k : 0;
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -205,11 +219,16 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
             const float* Dw = dwr + (which ? a.dw2o : a.dw1o);
             const float* Cm = which ? a.C2 : a.C1;
-            x[u] = load4_guard(Dw, i, r, bv && cv, vec);
-            y[u].x = (cv && kv && i < r) ? Cm[(int64_t)i * m + kc] : 0.f;
-            y[u].y = (cv && kv && i + 1 < r) ? Cm[(int64_t)(i + 1) * m + kc] : 0.f;
-            y[u].z = (cv && kv && i + 2 < r) ? Cm[(int64_t)(i + 2) * m + kc] : 0.f;
-            y[u].w = (cv && kv && i + 3 < r) ? Cm[(int64_t)(i + 3) * m + kc] : 0.f;
+            x[u] = load4_guard<VEC>(Dw, i, r, bv && cv);
+            // branch-free strided column loads (clamped row, select after)
+            const bool o0 = cv && kv && i < r, o1 = cv && kv && i + 1 < r;
+            const bool o2 = cv && kv && i + 2 < r, o3 = cv && kv && i + 3 < r;
+            const float c0 = Cm[(int64_t)(o0 ? i : 0) * m + kc], c1 = Cm[(int64_t)(o1 ? i + 1 : 0) * m + kc];
+            const float c2 = Cm[(int64_t)(o2 ? i + 2 : 0) * m + kc], c3 = Cm[(int64_t)(o3 ? i + 3 : 0) * m + kc];
+            y[u].x = o0 ? c0 : 0.f;
+            y[u].y = o1 ? c1 : 0.f;
+            y[u].z = o2 ? c2 : 0.f;
+            y[u].w = o3 ? c3 : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);

@@ -596,114 +596,137 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
 #define RAE_PRA 3            // workgroups per example for its A rows (+ 1 for its W rows)
 #endif
 // Partitioned data-parallel plans (StepArgs::privc): a rank owns ~1/G of each example's private
-// rows, so ONE workgroup per example takes them (waves 0-2 its A rows, wave 3 its W rows).
-__host__ __device__ inline int priv_wgs_per_example(int compact) { return compact ? 1 : RAE_PRA + 1; }
+// rows, so one WAVE per example takes them (its A rows, then its W rows): L / 4 workgroups.
+__host__ __device__ inline int priv_workgroups(int compact, int L) {
+    return compact ? (L + RAE_NWAVE - 1) / RAE_NWAVE : (RAE_PRA + 1) * L;
+}
+// the example's marked A / Ab rows wa0, wa0 + na, ... (bits of pmask words 0, 1)
 template <int OPT, bool V4, int Q, bool XY>
-__device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {
+__device__ __forceinline__ void priv_A_rows(const StepArgs& a, int b, int4 pm, const int32_t* dsc,
+                                            const float* rec, int wa0, int na, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int PRM = Q == 1 ? RAE_PRMAX : RAE_PRMAX / 2;
-    const int pwe = priv_wgs_per_example(a.privc);
-    const int b = t / pwe, sub = t - b * pwe;
-    // this wave's share: A rows (marked bits wa0, wa0 + na, ...) or W rows (wf0, wf0 + nf, ...)
-    const bool doA = a.privc ? w < RAE_NWAVE - 1 : sub < RAE_PRA;
-    const int wa0 = a.privc ? w : sub * RAE_NWAVE + w, na = a.privc ? RAE_NWAVE - 1 : RAE_NWAVE * RAE_PRA;
-    const int wf0 = a.privc ? 0 : w, nfw = a.privc ? 1 : RAE_NWAVE;
+    const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
+    // record j's entity id and coefficients (c_j, gamma_j) in lane j (NJ <= 64: plan)
+    const int sid = dsc[2 + (lane < NJ ? lane : 0)];
+    const float2 cg = reinterpret_cast<const float2*>(rec + a.lay.ocoef)[lane < NJ ? lane : 0];
+    // record vector of slot j: vec_0 = G1, vec_1 = G2 (bilinear) / V1, neg1 V1, neg2 V2
+    const int vo1 = XY ? a.vG2 : a.vV1;
+    const RecBuf rb_(a.vb);
+    const int rb0 = b * a.vbs;
+    uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
+    for (int i = 0; i < wa0; ++i) M &= M - 1;
+    while (M) {
+        int jr[PRM];
+        RowVec<V4, Q> pv[PRM], av[PRM], vv[PRM];
+        float ab[PRM], aab[PRM];
+#pragma unroll
+        for (int k = 0; k < PRM; ++k) {                   // a round: every load issued first
+            jr[k] = M ? __builtin_ctzll(M) : -1;
+            for (int i = 0; i < na; ++i) M &= M - 1;
+            if (jr[k] < 0) continue;
+            const int j = jr[k];
+            const int64_t e = __builtin_amdgcn_readlane(sid, j);
+            pv[k].load(a.A + e * r, nv, lane);
+            if (OPT == 0) av[k].load(a.aA + e * r, nv, lane); else av[k].zero();
+            const int vo = rb0 + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int c = lane + RAE_WAVE * q;
+                rb_.load(vv[k].v[q], (c < nv ? c : 0) * VW, vo);
+            }
+            ab[k] = a.Ab[e];
+            aab[k] = (OPT == 0) ? a.aAb[e] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < PRM; ++k) {
+            const int j = jr[k];
+            if (j < 0) continue;
+            const int64_t e = __builtin_amdgcn_readlane(sid, j);
+            const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.x), j));
+            const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.y), j));
+            RowVec<V4, Q> gr;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                vzero(gr.v[q]);
+                vfma(gr.v[q], cj, vv[k].v[q]);
+            }
+            apply_row<OPT, V4, Q>(a.A + e * r, (OPT == 0) ? a.aA + e * r : nullptr, pv[k], av[k],
+                                  gr, nv, a.lr, lane);
+            if (lane == 0) ab_update<OPT>(a, (int)e, ab[k], aab[k], gj);
+        }
+    }
+}
+// the example's marked W rows wf0, wf0 + nfw, ... (bits of pmask word 2)
+template <int OPT, bool V4, int Q>
+__device__ __forceinline__ void priv_W_rows(const StepArgs& a, int4 pm, const int32_t* dsc,
+                                            const float* rec, int wf0, int nfw, int lane) {
+    constexpr int VW = V4 ? 4 : 1;
+    constexpr int PRM = Q == 1 ? RAE_PRMAX : RAE_PRMAX / 2;
+    const int NJ = 2 + 2 * a.s, m = a.m, nv = m / VW;
+    const int p0 = dsc[1];
+    const int fid = dsc[2 + NJ + (lane < 32 ? lane : 0)];   // features 0..31 (privnf <= dcap)
+    typedef typename VecT<V4>::T VT;
+    const VT* rv = reinterpret_cast<const VT*>(rec);
+    VT ds[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int c = lane + RAE_WAVE * q;
+        ds[q] = rv[a.lay.odS / VW + (c < nv ? c : 0)];
+    }
+    unsigned M = (unsigned)pm.z;
+    for (int i = 0; i < wf0; ++i) M &= M - 1;
+    while (M) {
+        int fr[PRM];
+        RowVec<V4, Q> pv[PRM], av[PRM];
+        float xv[PRM];
+#pragma unroll
+        for (int k = 0; k < PRM; ++k) {
+            fr[k] = M ? __builtin_ctz(M) : -1;
+            for (int i = 0; i < nfw; ++i) M &= M - 1;
+            if (fr[k] < 0) continue;
+            const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
+            pv[k].load(a.W + f * m, nv, lane);
+            if (OPT == 0) av[k].load(a.aW + f * m, nv, lane); else av[k].zero();
+            xv[k] = a.values ? a.values[p0 + fr[k]] : 1.f;
+        }
+#pragma unroll
+        for (int k = 0; k < PRM; ++k) {
+            if (fr[k] < 0) continue;
+            const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
+            RowVec<V4, Q> gr;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) { vzero(gr.v[q]); vfma(gr.v[q], xv[k], ds[q]); }
+            apply_row<OPT, V4, Q>(a.W + f * m, (OPT == 0) ? a.aW + f * m : nullptr, pv[k], av[k],
+                                  gr, nv, a.lr, lane);
+        }
+    }
+}
+// private-row workgroup t, wave w: RAE_PRA workgroups per example for its A rows (wave i of them
+// the marked rows i, i + 4 RAE_PRA, ...) + one for its W rows (wave w: w, w + 4, ...); compact:
+// wave w of workgroup t takes every owned private row of example 4 t + w
+template <int OPT, bool V4, int Q, bool XY>
+__device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {
+    int b, sub;
+    if (a.privc) {
+        b = t * RAE_NWAVE + w;
+        sub = 0;
+        if (b >= a.L) return;
+    } else {
+        b = t / (RAE_PRA + 1);
+        sub = t - b * (RAE_PRA + 1);
+    }
     const int64_t slot = g % a.index_window;
     const int4 pm = reinterpret_cast<const int4*>(a.pmask)[slot * a.L + b];
     const int32_t* dsc = a.desc + (slot * a.dnx + b) * (int64_t)a.dstride;    // priv: dnx == L
     const float* rec = a.ex + (int64_t)b * a.lay.rec;
-    if (doA) {                                                // A / Ab rows
-        const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
-        // record j's entity id and coefficients (c_j, gamma_j) in lane j (NJ <= 64: plan)
-        const int sid = dsc[2 + (lane < NJ ? lane : 0)];
-        const float2 cg = reinterpret_cast<const float2*>(rec + a.lay.ocoef)[lane < NJ ? lane : 0];
-        // record vector of slot j: vec_0 = G1, vec_1 = G2 (bilinear) / V1, neg1 V1, neg2 V2
-        const int vo1 = XY ? a.vG2 : a.vV1;
-        const RecBuf rb_(a.vb);
-        const int rb0 = b * a.vbs;
-        // this wave's rows: marked bits wa0, wa0 + na, ...
-        uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
-        for (int i = 0; i < wa0; ++i) M &= M - 1;
-        while (M) {
-            int jr[PRM];
-            RowVec<V4, Q> pv[PRM], av[PRM], vv[PRM];
-            float ab[PRM], aab[PRM];
-#pragma unroll
-            for (int k = 0; k < PRM; ++k) {                   // a round: every load issued first
-                jr[k] = M ? __builtin_ctzll(M) : -1;
-                for (int i = 0; i < na; ++i) M &= M - 1;
-                if (jr[k] < 0) continue;
-                const int j = jr[k];
-                const int64_t e = __builtin_amdgcn_readlane(sid, j);
-                pv[k].load(a.A + e * r, nv, lane);
-                if (OPT == 0) av[k].load(a.aA + e * r, nv, lane); else av[k].zero();
-                const int vo = rb0 + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
-#pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    const int c = lane + RAE_WAVE * q;
-                    rb_.load(vv[k].v[q], (c < nv ? c : 0) * VW, vo);
-                }
-                ab[k] = a.Ab[e];
-                aab[k] = (OPT == 0) ? a.aAb[e] : 0.f;
-            }
-#pragma unroll
-            for (int k = 0; k < PRM; ++k) {
-                const int j = jr[k];
-                if (j < 0) continue;
-                const int64_t e = __builtin_amdgcn_readlane(sid, j);
-                const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.x), j));
-                const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cg.y), j));
-                RowVec<V4, Q> gr;
-#pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    vzero(gr.v[q]);
-                    vfma(gr.v[q], cj, vv[k].v[q]);
-                }
-                apply_row<OPT, V4, Q>(a.A + e * r, (OPT == 0) ? a.aA + e * r : nullptr, pv[k], av[k],
-                                      gr, nv, a.lr, lane);
-                if (lane == 0) ab_update<OPT>(a, (int)e, ab[k], aab[k], gj);
-            }
-        }
-    } else {                                                  // W rows
-        const int NJ = 2 + 2 * a.s, m = a.m, nv = m / VW;
-        const int nf = dsc[0], p0 = dsc[1];
-        const int fid = dsc[2 + NJ + (lane < 32 ? lane : 0)];   // features 0..31 (privnf <= dcap)
-        typedef typename VecT<V4>::T VT;
-        const VT* rv = reinterpret_cast<const VT*>(rec);
-        VT ds[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int c = lane + RAE_WAVE * q;
-            ds[q] = rv[a.lay.odS / VW + (c < nv ? c : 0)];
-        }
-        unsigned M = (unsigned)pm.z;
-        for (int i = 0; i < wf0; ++i) M &= M - 1;
-        (void)nf;
-        while (M) {
-            int fr[PRM];
-            RowVec<V4, Q> pv[PRM], av[PRM];
-            float xv[PRM];
-#pragma unroll
-            for (int k = 0; k < PRM; ++k) {
-                fr[k] = M ? __builtin_ctz(M) : -1;
-                for (int i = 0; i < nfw; ++i) M &= M - 1;
-                if (fr[k] < 0) continue;
-                const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
-                pv[k].load(a.W + f * m, nv, lane);
-                if (OPT == 0) av[k].load(a.aW + f * m, nv, lane); else av[k].zero();
-                xv[k] = a.values ? a.values[p0 + fr[k]] : 1.f;
-            }
-#pragma unroll
-            for (int k = 0; k < PRM; ++k) {
-                if (fr[k] < 0) continue;
-                const int64_t f = __builtin_amdgcn_readlane(fid, fr[k]);
-                RowVec<V4, Q> gr;
-#pragma unroll
-                for (int q = 0; q < Q; ++q) { vzero(gr.v[q]); vfma(gr.v[q], xv[k], ds[q]); }
-                apply_row<OPT, V4, Q>(a.W + f * m, (OPT == 0) ? a.aW + f * m : nullptr, pv[k], av[k],
-                                      gr, nv, a.lr, lane);
-            }
-        }
+    if (a.privc) {
+        priv_A_rows<OPT, V4, Q, XY>(a, b, pm, dsc, rec, 0, 1, lane);
+        priv_W_rows<OPT, V4, Q>(a, pm, dsc, rec, 0, 1, lane);
+    } else if (sub < RAE_PRA) {
+        priv_A_rows<OPT, V4, Q, XY>(a, b, pm, dsc, rec, sub * RAE_NWAVE + w, RAE_NWAVE * RAE_PRA, lane);
+    } else {
+        priv_W_rows<OPT, V4, Q>(a, pm, dsc, rec, w, RAE_NWAVE, lane);
     }
 }
 
