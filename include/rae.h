@@ -114,8 +114,8 @@ typedef struct rae_config {
                                * replicated update all of them, the partitioned one its own,   *
                                * one workgroup per example)                                     */
 #define RAE_PRIV_OFF 1        /* every row updated by the update launch                        */
-#define RAE_DPDENSE_AUTO 0    /* partials when they are no larger than dw1 / dw2 in the records  *
-                               * (per-rank partial chunk <= 2 r + 8 floats: l >~ relations)      */
+#define RAE_DPDENSE_AUTO 0    /* partials when they are at most half of dw1 / dw2 in the records *
+                               * (per-rank partial chunk <= r floats: l >~ 2 relations)          */
 #define RAE_DPDENSE_RECORDS 1 /* dw1 / dw2 of every example in the exchange records; the update *
                                * reduces dC1 / dC2 / dWb over the global batch (K = L)           */
 #define RAE_DPDENSE_PARTIALS 2 /* each rank reduces its own l examples' dC1 / dC2 / dWb before   *

@@ -90,6 +90,20 @@ __global__ __launch_bounds__(RAE_BT) void k_vrec(StepArgs a) {
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
+// bf16 shadow of R (RAE_RSHADOW): shadow = bf16(R), rounded as the M-tile staging rounds
+#ifndef RAE_RSHADOW
+#define RAE_RSHADOW 0
+#endif
+__global__ __launch_bounds__(256) void k_rshadow(StepArgs a) {
+    typedef __bf16 bf4_t __attribute__((ext_vector_type(4)));
+    const int64_t n4 = (int64_t)a.r * a.r * a.m / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 v = reinterpret_cast<const float4*>(a.R3)[i];
+        bf4_t q;
+        q[0] = (__bf16)v.x; q[1] = (__bf16)v.y; q[2] = (__bf16)v.z; q[3] = (__bf16)v.w;
+        reinterpret_cast<bf4_t*>(a.Rsh)[i] = q;
+    }
+}
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -161,9 +175,17 @@ __global__ __launch_bounds__(256) void k_cwarm(StepArgs a) {
     const float4* c1 = reinterpret_cast<const float4*>(a.C1);
     const float4* c2 = reinterpret_cast<const float4*>(a.C2);
     float acc = 0.f;
-    for (int i = part * 256 + threadIdx.x; i < 2 * n4; i += per * 256) {
-        const float4 v = i < n4 ? c1[i] : c2[i - n4];
-        acc += v.x + v.y + v.z + v.w;
+    const int stride = per * 256;
+    for (int i0 = part * 256 + threadIdx.x; i0 < 2 * n4; i0 += 8 * stride) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {                // eight loads in flight per thread
+            const int i = i0 + u * stride;
+            const int ic = i < 2 * n4 ? i : 0;
+            v[u] = ic < n4 ? c1[ic] : c2[ic - n4];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
     }
     if (acc == 1.2345e-30f) a.err[1] = 1;     // keeps the loads live; never true in practice
 }
@@ -641,9 +663,11 @@ static int wire_records(const rae_config& c) {
     if (c.decoder != RAE_DEC_SP || c.world_size <= 1) return 0;
     if (c.dp_dense == RAE_DPDENSE_RECORDS) return 1;
     if (c.dp_dense == RAE_DPDENSE_PARTIALS) return 2;
+    // partials when their chunk is at most half of dw1 / dw2 (l >~ 2 m): below that they move
+    // about as many bytes and k_dpart (~4 us at C3, l = 100) sits on the critical path
     const int pc = align4((dense_partial_floats(c.embed, c.relations) + c.batch_size - 1) /
                           c.batch_size);
-    return pc <= 2 * align4(c.embed) + 8 ? 2 : 1;
+    return pc <= align4(c.embed) ? 2 : 1;
 }
 extern "C" int64_t rae_exchange_record_floats(const rae_config* cfg) {
     if (!cfg) return -1;
@@ -893,6 +917,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
+    // bf16 shadow of R for the M-tile passes: bf16 blocks (m <= 128, m % 4 == 0) whose R update runs
+    // the LDS tile task (the only writer of R then keeps the shadow current)
+    const bool rsh = RAE_RSHADOW && a.bf16 && c.relations <= 128 && c.relations % 4 == 0 &&
+                     bil_rows_lds_bytes(c.relations, true, c.optimizer == RAE_OPT_ADAGRAD) > 0;
+    const size_t o_rsh = rsh ? take(2ull * c.embed * c.embed * c.relations) : 0;
     const size_t o_vb = a.lay.wire ? take(4ull * a.vbs * L) : 0;
     const size_t o_dwb = a.dpart ? take(4ull * a.dws * L) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
@@ -939,6 +968,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
     if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
     if (a.dpart) a.dwb = reinterpret_cast<float*>(p->ws + o_dwb);
+    a.Rsh = rsh ? reinterpret_cast<__bf16*>(p->ws + o_rsh) : nullptr;
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -1221,6 +1251,8 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     if (count == 0) return RAE_OK;
     hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 3), dim3(RAE_FBT), p->smem_idx, st,
                        p->args, first);
+    if (p->args.Rsh)          // the shadow from the parameters as they are before these steps
+        hipLaunchKernelGGL(k_rshadow, dim3(2048), dim3(256), 0, st, p->args);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, p->args, first);
     HIPCHK(hipGetLastError());

@@ -51,10 +51,10 @@ def test_struct_layout_matches_header(built_lib):
     part = ((2 * 100 + 4 + ((2 * 42 + 3) & ~3) + 1 + 3) & ~3) + pc
     assert (pc, part) == (404, 696)
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == part
-    cfg.dp_dense = 0                 # auto: partials when no larger than dw1 / dw2 (l ~ m here)
-    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == part
-    cfg.batch_size = 40              # l << m: dw1 / dw2 are the smaller record
+    cfg.dp_dense = 0                 # auto: records at l ~ m (the partials would move as much) ...
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == wire
+    cfg.batch_size = 1024            # ... partials at l >> m: 40 floats of partial block each
+    assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == 292 + 40
     cfg.batch_size = 100
     cfg.decoder = 1     # the bilinear decoders exchange their whole record
     assert built_lib.rae_exchange_record_floats(C.byref(cfg)) == \

@@ -107,12 +107,12 @@ def test_partitioned_update_equals_global_batch(tmp_path, decoder, ws):
 @pytest.mark.parametrize("decoder,ws,dense", [("sp", 2, "auto"), ("rescal", 2, "auto"),
                                               ("rescal+sp", 2, "auto"), ("sp", 4, "auto"),
                                               ("sp", 8, "auto"), ("rescal+sp", 8, "auto"),
-                                              ("sp", 2, "records"), ("sp", 4, "records"),
-                                              ("sp", 8, "records")])
+                                              ("sp", 2, "partials"), ("sp", 4, "partials"),
+                                              ("sp", 8, "partials")])
 def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws, dense):
     """The HIP path on `ws` ranks sharing the GPU (replicated update) == the oracle at the
     global batch, replicas bit-identical; SP both ways of moving the dense decoder-matrix
-    gradients (rae.h RAE_DPDENSE_*: auto = each rank's partials at this shape, or every
+    gradients (rae.h RAE_DPDENSE_*: each rank's partials, or -- auto at this shape -- every
     example's dw1 / dw2 in the records)."""
     _launch(["gpu", str(tmp_path), decoder, "replicated", dense], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
@@ -128,7 +128,8 @@ def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws
 @pytest.mark.gpu
 @pytest.mark.parametrize("decoder,ws,dense", [("sp", 2, "auto"), ("rescal+sp", 2, "auto"),
                                               ("sp", 4, "auto"), ("rescal", 4, "auto"),
-                                              ("sp", 8, "auto"), ("sp", 4, "records")])
+                                              ("sp", 8, "auto"), ("sp", 4, "partials"),
+                                              ("sp", 8, "partials")])
 def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dense):
     """The HIP path with the row-owner partitioned update (k_build_dplists, k_dp_move, the
     owned-rows row index) on `ws` ranks sharing the GPU: == the oracle at the global batch,
