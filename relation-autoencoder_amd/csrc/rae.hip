@@ -90,20 +90,6 @@ __global__ __launch_bounds__(RAE_BT) void k_vrec(StepArgs a) {
 }
 
 // ---- RESCAL / RESCAL+SP forward phase (rae_bilinear.hpp) ----
-// bf16 shadow of R (RAE_RSHADOW): shadow = bf16(R), rounded as the M-tile staging rounds
-#ifndef RAE_RSHADOW
-#define RAE_RSHADOW 0
-#endif
-__global__ __launch_bounds__(256) void k_rshadow(StepArgs a) {
-    typedef __bf16 bf4_t __attribute__((ext_vector_type(4)));
-    const int64_t n4 = (int64_t)a.r * a.r * a.m / 4;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-        const float4 v = reinterpret_cast<const float4*>(a.R3)[i];
-        bf4_t q;
-        q[0] = (__bf16)v.x; q[1] = (__bf16)v.y; q[2] = (__bf16)v.z; q[3] = (__bf16)v.w;
-        reinterpret_cast<bf4_t*>(a.Rsh)[i] = q;
-    }
-}
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_bil_enc(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -161,33 +147,6 @@ __global__ __launch_bounds__(RAE_FINT) void k_bil_fin(StepArgs a) {
     __shared__ float smt[4 * 1024];      // M-tile half sums, r <= 1024
     __shared__ float red[2 * RAE_FINW];
     bil_finish(a, blockIdx.x, sdp, smt, red);
-}
-
-// A/B knob (profiles/r04_ab.txt): a launch in front of the SP forward whose
-// RAE_CWARM workgroups per XCD (workgroup x runs on XCD x % 8) read C1 and C2 once, so the forward's
-// 100 example workgroups find the decoder matrices in their XCD's L2 (0: off, the product form)
-#ifndef RAE_CWARM
-#define RAE_CWARM 0
-#endif
-__global__ __launch_bounds__(256) void k_cwarm(StepArgs a) {
-    const int per = gridDim.x / 8, part = blockIdx.x / 8;
-    const int n4 = a.r * a.m / 4;
-    const float4* c1 = reinterpret_cast<const float4*>(a.C1);
-    const float4* c2 = reinterpret_cast<const float4*>(a.C2);
-    float acc = 0.f;
-    const int stride = per * 256;
-    for (int i0 = part * 256 + threadIdx.x; i0 < 2 * n4; i0 += 8 * stride) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {                // eight loads in flight per thread
-            const int i = i0 + u * stride;
-            const int ic = i < 2 * n4 ? i : 0;
-            v[u] = ic < n4 ? c1[ic] : c2[ic - n4];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
-    }
-    if (acc == 1.2345e-30f) a.err[1] = 1;     // keeps the loads live; never true in practice
 }
 
 // shapes with compile-time specialisations of the forward kernel (BASELINE.json configs
@@ -300,7 +259,9 @@ __host__ __device__ constexpr int update_lds_floats() {
 
 // wg0 / ngrid: this workgroup's index and the number of workgroups of the update's own grid
 // (the fused bilinear kernel puts the update's workgroups in front of the R-tile ones)
-template <int OPT, bool V4, int Q, bool BIL>
+// VS: where the A-row tasks find the record vectors (rae_update.hpp entity_accum): 0 SP records
+// (single rank), 1 bilinear records, 2 the SP wire record's vector buffer (data parallel)
+template <int OPT, bool V4, int Q, int VS>
 __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngrid, float* lds) {
     typedef typename VecT<V4>::T VT;
     constexpr int kF = update_lds_floats<V4, Q>() - RAE_NWAVE;
@@ -319,7 +280,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         const int nX = priv_workgroups(a.privc, a.L);
         const int x = RAE_PRIV_LAST ? wgp - (ngrid - nX) : wgp;
         if (x >= 0 && x < nX) {
-            task_private_rows<OPT, V4, Q, BIL>(a, g, x, w, lane);
+            task_private_rows<OPT, V4, Q, VS>(a, g, x, w, lane);
             return;
         }
         if (!RAE_PRIV_LAST) wgp -= nX;
@@ -353,7 +314,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
 #endif
     if (wg < nT) {                                            // dense tiles
         RAE_FIRST(wg < nCt ? 0 : 2);
-        if (a.dpart) {                   // dense partials: the ranks' sums (wave 0), no K chain
+        if (VS == 2 && a.dpart) {        // dense partials: the ranks' sums (wave 0), no K chain
             if (w == 0) {
                 if (wg < nCt) {
                     const int which = wg / (rt * mt), ti = wg - which * rt * mt;
@@ -379,11 +340,10 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         RAE_WAVE_END();
         return;
     }
-    if (wg < nT + nP) {                                       // the cost
-        const int t = (wg - nT) * RAE_NWAVE + w;
-        if (t == 0) {
+    if (wg < nT + nP) {                                       // the cost (one workgroup)
+        if (wg == nT) {
             RAE_FIRST(3);
-            task_cost(a, lane);
+            task_cost(a, w, lane, reinterpret_cast<double*>(lds));
         }
         RAE_WAVE_END();
         return;
@@ -399,7 +359,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         const bool isA = seg.x >= 0;
         RAE_FIRST(isA ? 8 : 9);
         if (isA) {
-            wg_entity_row<OPT, V4, Q, BIL>(a, slot, seg, w, lane, spart, sgb);
+            wg_entity_row<OPT, V4, Q, VS>(a, slot, seg, w, lane, spart, sgb);
         } else {
             seg.x = ~seg.x;
             wg_feature_row<OPT, V4, Q>(a, ex0, slot, seg, w, lane, spart);
@@ -421,7 +381,7 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         const bool curA = cur.x >= 0;
         if (!curA) cur.x = ~cur.x;
         RAE_FIRST((curA ? 4 : 5) + (cur.z - cur.y > RAE_HEAVY ? 2 : 0));
-        if (curA) task_entity_row<OPT, V4, Q, BIL>(a, slot, cur, lane);
+        if (curA) task_entity_row<OPT, V4, Q, VS>(a, slot, cur, lane);
         else task_feature_row<OPT, V4, Q>(a, ex0, slot, cur, lane);
         RAE_WAVE_END();
     }
@@ -434,34 +394,27 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
 #else
 #define RAE_UPD_ATTR
 #endif
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool WIRE>
 __global__ __launch_bounds__(RAE_BT) RAE_UPD_ATTR void k_update(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
-    update_body<OPT, V4, Q, false>(a, blockIdx.x, gridDim.x, lds);
+    update_body<OPT, V4, Q, WIRE ? 2 : 0>(a, blockIdx.x, gridDim.x, lds);
 }
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) void k_update_bil(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
-    update_body<OPT, V4, Q, true>(a, blockIdx.x, gridDim.x, lds);
+    update_body<OPT, V4, Q, 1>(a, blockIdx.x, gridDim.x, lds);
 }
 // The bilinear decoders' update phase in ONE launch: workgroups [0, gu) run k_update_bil's tasks
 // (Wb tiles, cost, A / W rows: latency-bound chains), the rest k_bil_rows' R tiles (16 rows
 // (i, j) x all m per wave: the HBM-heavy R sweep) -- the two have no data in common, so the
 // row chains run under the R sweep instead of after it.  Dynamic LDS: the R tiles' (DMA'd R and
 // accumulator rows); an update workgroup carves its partials from the same allocation.
-#ifndef RAE_BIL_RT_FIRST
-#define RAE_BIL_RT_FIRST 0    // A/B knob: the R-tile workgroups dispatched ahead of the update's
-#endif
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
-    if (RAE_BIL_RT_FIRST) {                  // physical order: R tiles, then the update's tasks
-        const int nr = gridDim.x - gu;
-        wg = wg < nr ? gu + wg : wg - nr;
-    }
+    const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (wg < gu) {
-        update_body<OPT, V4, Q, true>(a, wg, gu, reinterpret_cast<float*>(smem));
+        update_body<OPT, V4, Q, 1>(a, wg, gu, reinterpret_cast<float*>(smem));
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -917,11 +870,6 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
-    // bf16 shadow of R for the M-tile passes: bf16 blocks (m <= 128, m % 4 == 0) whose R update runs
-    // the LDS tile task (the only writer of R then keeps the shadow current)
-    const bool rsh = RAE_RSHADOW && a.bf16 && c.relations <= 128 && c.relations % 4 == 0 &&
-                     bil_rows_lds_bytes(c.relations, true, c.optimizer == RAE_OPT_ADAGRAD) > 0;
-    const size_t o_rsh = rsh ? take(2ull * c.embed * c.embed * c.relations) : 0;
     const size_t o_vb = a.lay.wire ? take(4ull * a.vbs * L) : 0;
     const size_t o_dwb = a.dpart ? take(4ull * a.dws * L) : 0;
     const size_t o_pfr = a.bf16 ? take(16ull * (a.Lp / 32) * ((c.relations + 15) / 16) * 64) : 0;
@@ -968,7 +916,6 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
     if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
     if (a.dpart) a.dwb = reinterpret_cast<float*>(p->ws + o_dwb);
-    a.Rsh = rsh ? reinterpret_cast<__bf16*>(p->ws + o_rsh) : nullptr;
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
@@ -1109,8 +1056,6 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
     }
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;
     const bool c2 = a.m == 30 && a.r == 100 && a.s == 10;
-    if (RAE_CWARM > 0 && p->v4)
-        RAE_LAUNCH(p, k_cwarm, dim3(8 * RAE_CWARM), dim3(256), 0, st, a);
     if (c3 && p->v4)
         RAE_LAUNCH(p, (k_forward<true, DimsC3>), gr, bt, p->smem_fwd, st, a);
     else if (c2 && !p->v4)
@@ -1198,8 +1143,15 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
         else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
     } else {
-        if (p->q == 1) RAE_LAUNCH(p, (k_update<OPT, V4, 1>), gu, bt, 0, st, a);
-        else RAE_LAUNCH(p, (k_update<OPT, V4, 2>), gu, bt, 0, st, a);
+        // the data-parallel SP update (wire records: vectors in the vector buffer, dense
+        // partials) and the single-rank one are separate instantiations
+        if (a.lay.wire) {
+            if (p->q == 1) RAE_LAUNCH(p, (k_update<OPT, V4, 1, true>), gu, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_update<OPT, V4, 2, true>), gu, bt, 0, st, a);
+        } else {
+            if (p->q == 1) RAE_LAUNCH(p, (k_update<OPT, V4, 1, false>), gu, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_update<OPT, V4, 2, false>), gu, bt, 0, st, a);
+        }
     }
 }
 template <int OPT, bool V4>
@@ -1251,8 +1203,6 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     if (count == 0) return RAE_OK;
     hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 3), dim3(RAE_FBT), p->smem_idx, st,
                        p->args, first);
-    if (p->args.Rsh)          // the shadow from the parameters as they are before these steps
-        hipLaunchKernelGGL(k_rshadow, dim3(2048), dim3(256), 0, st, p->args);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, p->args, first);
     HIPCHK(hipGetLastError());

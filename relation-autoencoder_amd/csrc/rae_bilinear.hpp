@@ -284,36 +284,6 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     // ---- stage: LDS row (ii, jj) = R[i0+ii][j0+jj][0..m); rows past r are zero
     if (DIRECT) {
         // no staging: the MFMA chains read the block's rows from global memory
-    } else if (BF16 && a.Rsh && (m & 3) == 0) {
-        // from the bf16 shadow: 8-byte runs of 4 elements, already rounded
-        typedef __bf16 bf4_t __attribute__((ext_vector_type(4)));
-        const int m4 = m / 4, nv = RAE_MTI * RAE_MTJ * m4;
-        for (int e0 = 0; e0 < nv; e0 += RAE_MTT * RAE_MT_SB) {
-            bf4_t v[RAE_MT_SB];
-#pragma unroll
-            for (int u = 0; u < RAE_MT_SB; ++u) {
-                const int e = e0 + u * RAE_MTT + tid;
-                const int row = e / m4, kq = e - row * m4;
-                const int i = i0 + row / RAE_MTJ, j = j0 + row % RAE_MTJ;
-                const bool ok = e < nv && i < r && j < r;
-                const bf4_t x = *reinterpret_cast<const bf4_t*>(
-                    a.Rsh + ((int64_t)(ok ? i : 0) * r + (ok ? j : 0)) * m + 4 * kq);
-                const bf4_t z = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-                v[u] = ok ? x : z;
-            }
-#pragma unroll
-            for (int u = 0; u < RAE_MT_SB; ++u) {
-                const int e = e0 + u * RAE_MTT + tid;
-                if (e < nv) {
-                    const int row = e / m4, kq = e - row * m4;
-                    *reinterpret_cast<bf4_t*>(reinterpret_cast<__bf16*>(smem) + row * ST + 4 * kq) = v[u];
-                    if (tr) {
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) sT[(4 * kq + c) * RAE_MT_TP + row] = v[u][c];
-                    }
-                }
-            }
-        }
     } else if ((m & 3) == 0) {
         const int m4 = m / 4, nv = RAE_MTI * RAE_MTJ * m4;
         for (int e0 = 0; e0 < nv; e0 += RAE_MTT * RAE_MT_SB) {
@@ -1435,12 +1405,6 @@ __device__ void task_bilinear_rows_lds(const StepArgs& a, int ijt, int slot, int
         }
         *reinterpret_cast<float4*>(a.R3 + base + lo) = w;
         if constexpr (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + base + lo) = ac;
-        if (a.Rsh) {                                      // keep the bf16 shadow = bf16(R)
-            typedef __bf16 bf4_t __attribute__((ext_vector_type(4)));
-            bf4_t q;
-            q[0] = (__bf16)w.x; q[1] = (__bf16)w.y; q[2] = (__bf16)w.z; q[3] = (__bf16)w.w;
-            *reinterpret_cast<bf4_t*>(a.Rsh + base + lo) = q;
-        }
     }
     if (reg) {
         const double L1 = wave_sum_d((double)l1), L2 = wave_sum_d((double)l2);

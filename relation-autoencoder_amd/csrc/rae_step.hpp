@@ -132,10 +132,6 @@ struct StepArgs {
     float* dwb;
     int dws, dw1o, dw2o;
     int dpart;           // dense partials (RecLayout wire 2)
-    // bf16 shadow of R / C (r, r, m) for the M-tile passes (RAE_RSHADOW): refreshed from R with every
-    // row-index build, then kept equal to bf16(R) by the R update -- the passes stage 2-byte
-    // elements instead of converting 4-byte ones (the same RNE rounding: bit-identical operands)
-    __bf16* Rsh;
     // row index of the global batches (rae_index.hpp), one slot per batch % index_window
     int HA, HW, RA, RW, posbits;
     int64_t index_window;

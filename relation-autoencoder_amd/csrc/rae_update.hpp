@@ -253,11 +253,32 @@ __device__ void tile_from_partials(const StepArgs& a, float* M, float* aM, int n
 }
 
 // ---- the batch cost: -mean(all_scores) = -(sum_b loss_b) / (4L + 2Ls)  (OieModel.py:90)
-__device__ void task_cost(const StepArgs& a, int lane) {
-    double loss = 0.0;
-    for (int b = lane; b < a.L; b += RAE_WAVE)
-        loss += (double)a.ex[(int64_t)b * a.lay.rec + a.lay.oloss];
+// One workgroup: wave w sums examples [w q, (w + 1) q) of the global batch with eight loads in
+// flight per lane (eight chains, combined in a fixed order), the four wave sums combined in wave
+// order -- a fixed summation order; at L = 8192 a single lane-strided chain was 128 dependent
+// round trips, the partitioned update's tail.
+__device__ void task_cost(const StepArgs& a, int w, int lane, double* sred) {
+    const int q = (a.L + RAE_NWAVE - 1) / RAE_NWAVE;
+    const int b0 = min(w * q, a.L), b1 = min(b0 + q, a.L);
+    double t[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int c = b0 + lane; c < b1; c += 8 * RAE_WAVE) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int b = c + u * RAE_WAVE;
+            v[u] = a.ex[(int64_t)(b < b1 ? b : b0) * a.lay.rec + a.lay.oloss];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] += c + u * RAE_WAVE < b1 ? (double)v[u] : 0.0;
+    }
+    double loss = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     loss = wave_sum_d(loss);
+    if (lane == 0) sred[w] = loss;
+    __syncthreads();
+    if (w != 0) return;
+    loss = sred[0];
+#pragma unroll
+    for (int ww = 1; ww < RAE_NWAVE; ++ww) loss += sred[ww];
     if (lane == 0) {
         const double D = 4.0 * a.L + 2.0 * a.L * a.s;
         const float cost = (float)(-loss / D);
@@ -322,16 +343,22 @@ __device__ __forceinline__ void apply_row(float* p, float* acc, RowVec<V4, Q>& p
 // vectors are loaded UNR at a time with every load issued before the first FMA.
 // entity_accum: records [st, en) of the slot's sorted list into g (lane-strided row) and gb
 // (this lane's share of the Ab gradient); rec0 = the record of a one-record row.
-template <bool V4, int Q, bool XY>
+// VS: where the record vectors are -- 0: SP records, 1: bilinear records (e2 has its own G2),
+// 2: the SP wire record's vector buffer (StepArgs::vb; data parallel).  0 / 1 address them with
+// the record offsets at compile-time-known fields (the single-rank hot path's code).
+template <bool V4, int Q, int VS>
 __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, int st, int en,
                                              int rec0, RowVec<V4, Q>& g, float& gb, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int UNR = Q == 1 ? RAE_UNR1 : 2;
     constexpr int UNRH = Q == 1 ? RAE_UNRH : RAE_UNRH / 2;
+    constexpr bool XY = VS == 1, EXT = VS == 2;
     typedef typename VecT<V4>::T VT;
     const int nv = a.r / VW, s = a.s, NJ = 2 + 2 * s;
-    const int vo1 = XY ? a.vG2 : a.vV1;           // SP: e2 has no A gradient (c = 0)
-    const RecBuf rb_(a.vb);                       // the record vectors (rae_step.hpp vb)
+    const int oG1 = EXT ? a.vG1 : a.lay.oG1, oV1 = EXT ? a.vV1 : a.lay.oV1;
+    const int oV2 = EXT ? a.vV2 : a.lay.oV2;
+    const int vo1 = XY ? a.lay.oG2 : oV1;         // SP: e2 has no A gradient (c = 0)
+    const RecBuf rb_(EXT ? a.vb : a.ex);          // the record vectors (rae_step.hpp vb)
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
         // a one-record row's record rides in its segment: no srec round trip
@@ -343,7 +370,7 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
         const float ga = er[1];
         if (lane >= n) cj = 0.f;
         gb += lane < n ? ga : 0.f;
-        const int vo = b * a.vbs + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
+        const int vo = (EXT ? b * a.vbs : rb) + (j == 0 ? oG1 : (j == 1 ? vo1 : (j < 2 + s ? oV1 : oV2)));
         // one round: U record vectors loaded (all issued before the first FMA), then summed
         // in record order -- the same order for every U, so the round width is free
         auto round = [&](auto Uc, int k0) {
@@ -385,7 +412,7 @@ __device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, f
     if (OPT == 0) a.aAb[e] = ac;
 }
 
-template <int OPT, bool V4, int Q, bool XY>
+template <int OPT, bool V4, int Q, int VS>
 __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     const int r = a.r, nv = r / VW;
@@ -406,7 +433,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
     g.zero();
     float gb = 0.f;
-    entity_accum<V4, Q, XY>(a, base, seg.y, seg.z, seg.w, g, gb, lane);
+    entity_accum<V4, Q, VS>(a, base, seg.y, seg.z, seg.w, g, gb, lane);
     gb = wave_sum(gb);
     apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
     if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb);
@@ -415,7 +442,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
 // A very heavy row (> RAE_VHEAVY records) per workgroup: its sorted record list split into
 // four contiguous chunks, one per wave; wave 0 sums the partial rows in wave order and applies
 // the update (its parameter loads in flight meanwhile).  spart: RAE_NWAVE * 64 * Q vectors.
-template <int OPT, bool V4, int Q, bool XY>
+template <int OPT, bool V4, int Q, int VS>
 __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, int lane,
                               typename VecT<V4>::T* spart, float* sgb) {
     constexpr int VW = V4 ? 4 : 1;
@@ -436,7 +463,7 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
     }
     g.zero();
     float gb = 0.f;
-    if (c0 < c1) entity_accum<V4, Q, XY>(a, base, c0, c1, seg.w, g, gb, lane);
+    if (c0 < c1) entity_accum<V4, Q, VS>(a, base, c0, c1, seg.w, g, gb, lane);
     gb = wave_sum(gb);
 #pragma unroll
     for (int q = 0; q < Q; ++q) spart[(w * Q + q) * RAE_WAVE + lane] = g.v[q];
@@ -601,19 +628,22 @@ __host__ __device__ inline int priv_workgroups(int compact, int L) {
     return compact ? (L + RAE_NWAVE - 1) / RAE_NWAVE : (RAE_PRA + 1) * L;
 }
 // the example's marked A / Ab rows wa0, wa0 + na, ... (bits of pmask words 0, 1)
-template <int OPT, bool V4, int Q, bool XY>
+template <int OPT, bool V4, int Q, int VS>
 __device__ __forceinline__ void priv_A_rows(const StepArgs& a, int b, int4 pm, const int32_t* dsc,
                                             const float* rec, int wa0, int na, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     constexpr int PRM = Q == 1 ? RAE_PRMAX : RAE_PRMAX / 2;
+    constexpr bool XY = VS == 1, EXT = VS == 2;
     const int s = a.s, NJ = 2 + 2 * s, r = a.r, nv = r / VW;
     // record j's entity id and coefficients (c_j, gamma_j) in lane j (NJ <= 64: plan)
     const int sid = dsc[2 + (lane < NJ ? lane : 0)];
     const float2 cg = reinterpret_cast<const float2*>(rec + a.lay.ocoef)[lane < NJ ? lane : 0];
     // record vector of slot j: vec_0 = G1, vec_1 = G2 (bilinear) / V1, neg1 V1, neg2 V2
-    const int vo1 = XY ? a.vG2 : a.vV1;
-    const RecBuf rb_(a.vb);
-    const int rb0 = b * a.vbs;
+    const int oG1 = EXT ? a.vG1 : a.lay.oG1, oV1 = EXT ? a.vV1 : a.lay.oV1;
+    const int oV2 = EXT ? a.vV2 : a.lay.oV2;
+    const int vo1 = XY ? a.lay.oG2 : oV1;
+    const RecBuf rb_(EXT ? a.vb : a.ex);
+    const int rb0 = b * (EXT ? a.vbs : a.lay.rec);
     uint64_t M = ((uint64_t)(uint32_t)pm.y << 32) | (uint32_t)pm.x;
     for (int i = 0; i < wa0; ++i) M &= M - 1;
     while (M) {
@@ -629,7 +659,7 @@ __device__ __forceinline__ void priv_A_rows(const StepArgs& a, int b, int4 pm, c
             const int64_t e = __builtin_amdgcn_readlane(sid, j);
             pv[k].load(a.A + e * r, nv, lane);
             if (OPT == 0) av[k].load(a.aA + e * r, nv, lane); else av[k].zero();
-            const int vo = rb0 + (j == 0 ? a.vG1 : (j == 1 ? vo1 : (j < 2 + s ? a.vV1 : a.vV2)));
+            const int vo = rb0 + (j == 0 ? oG1 : (j == 1 ? vo1 : (j < 2 + s ? oV1 : oV2)));
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const int c = lane + RAE_WAVE * q;
@@ -705,10 +735,11 @@ __device__ __forceinline__ void priv_W_rows(const StepArgs& a, int4 pm, const in
 // private-row workgroup t, wave w: RAE_PRA workgroups per example for its A rows (wave i of them
 // the marked rows i, i + 4 RAE_PRA, ...) + one for its W rows (wave w: w, w + 4, ...); compact:
 // wave w of workgroup t takes every owned private row of example 4 t + w
-template <int OPT, bool V4, int Q, bool XY>
+template <int OPT, bool V4, int Q, int VS>
 __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, int lane) {
     int b, sub;
-    if (a.privc) {
+    const bool compact = VS != 0 && a.privc;       // VS 0: the single-rank SP plan, never compact
+    if (compact) {
         b = t * RAE_NWAVE + w;
         sub = 0;
         if (b >= a.L) return;
@@ -720,11 +751,11 @@ __device__ void task_private_rows(const StepArgs& a, int64_t g, int t, int w, in
     const int4 pm = reinterpret_cast<const int4*>(a.pmask)[slot * a.L + b];
     const int32_t* dsc = a.desc + (slot * a.dnx + b) * (int64_t)a.dstride;    // priv: dnx == L
     const float* rec = a.ex + (int64_t)b * a.lay.rec;
-    if (a.privc) {
-        priv_A_rows<OPT, V4, Q, XY>(a, b, pm, dsc, rec, 0, 1, lane);
+    if (compact) {
+        priv_A_rows<OPT, V4, Q, VS>(a, b, pm, dsc, rec, 0, 1, lane);
         priv_W_rows<OPT, V4, Q>(a, pm, dsc, rec, 0, 1, lane);
     } else if (sub < RAE_PRA) {
-        priv_A_rows<OPT, V4, Q, XY>(a, b, pm, dsc, rec, sub * RAE_NWAVE + w, RAE_NWAVE * RAE_PRA, lane);
+        priv_A_rows<OPT, V4, Q, VS>(a, b, pm, dsc, rec, sub * RAE_NWAVE + w, RAE_NWAVE * RAE_PRA, lane);
     } else {
         priv_W_rows<OPT, V4, Q>(a, pm, dsc, rec, w, RAE_NWAVE, lane);
     }
