@@ -217,6 +217,12 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_ROWPCT
 #define RAE_ROWPCT 100        // row-task waves per 100 dispatch-table capacity entries
 #endif
+#ifndef RAE_HCH
+#define RAE_HCH 128           // very heavy rows above this many records are split into chunks
+#endif
+#ifndef RAE_HCH_MINL
+#define RAE_HCH_MINL 256      // ... in plans with a global batch of at least this many examples
+#endif
 #ifndef RAE_NVC_MIN
 #define RAE_NVC_MIN 32
 #endif
@@ -427,6 +433,12 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
 #ifndef RAE_BIL_FUSED_UPD
 #define RAE_BIL_FUSED_UPD 1   // bilinear update phase as one launch (k_bil_update)
 #endif
+
+// rows split into chunks (StepArgs::hch): each row's chunk sums combined in order + its update
+template <int OPT, bool V4, int Q>
+__global__ __launch_bounds__(RAE_BT) void k_heavy_fin(StepArgs a) {
+    heavy_fin<OPT, V4, Q>(a, blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6), threadIdx.x & 63);
+}
 
 // Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,
 // reset the scratch, L1/L2 partials of the old W per block (fixed grid -> deterministic).
@@ -807,9 +819,20 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         const int Lo = a.part ? (L + a.G - 1) / a.G : L;     // the rows this rank updates
         const int nvc = Lo / RAE_NVC_DIV > RAE_NVC_MIN ? Lo / RAE_NVC_DIV : RAE_NVC_MIN;
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
+        // large global batches: very heavy rows with more than RAE_HCH records split into
+        // chunks (every chunk a workgroup task: they need NVC >= all chunks of a batch)
+        a.hch = L >= RAE_HCH_MINL ? RAE_HCH : 0;
+        if (a.hch) {
+            a.HF = (a.RA + a.RW) / a.hch + 1;
+            if (a.NVC < a.HF + 1) a.NVC = a.HF + 1;
+            a.hps = ((c.embed + 3) & ~3) + 4 > ((c.relations + 3) & ~3) ? ((c.embed + 3) & ~3) + 4
+                                                                       : ((c.relations + 3) & ~3);
+        }
     }
     const size_t o_thdr = take(16 * W_), o_task = take(16ull * W_ * a.TC);
     const size_t o_vtask = take(16ull * W_ * a.NVC);
+    const size_t o_hfin = a.hch ? take(16ull * W_ * a.HF) : 0;
+    const size_t o_hpart = a.hch ? take(4ull * a.NVC * a.hps) : 0;
     {
         const int NJd = 2 + 2 * c.neg_samples;
         int cap = c.max_row_nnz > 0 ? c.max_row_nnz : 1;
@@ -897,6 +920,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.thdr = reinterpret_cast<int32_t*>(p->ws + o_thdr);
     a.task = reinterpret_cast<int32_t*>(p->ws + o_task);
     a.vtask = reinterpret_cast<int32_t*>(p->ws + o_vtask);
+    a.hfin = a.hch ? reinterpret_cast<int32_t*>(p->ws + o_hfin) : nullptr;
+    a.hpart = a.hch ? reinterpret_cast<float*>(p->ws + o_hpart) : nullptr;
 
     a.desc = reinterpret_cast<int32_t*>(p->ws + o_desc);
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
@@ -1180,6 +1205,27 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     if (a.opt == RAE_OPT_ADAGRAD) launch_update_q<0>(p, gu, bt, st, a);
     else launch_update_q<1>(p, gu, bt, st, a);
     HIPCHK(hipGetLastError());
+    if (a.hch) {              // the rows split into chunks: their chunk sums combined + updated
+        const dim3 gh(ceil_div(a.HF, RAE_NWAVE));
+        if (a.opt == RAE_OPT_ADAGRAD) {
+            if (p->v4) {
+                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, true, 1>), gh, bt, 0, st, a);
+                else RAE_LAUNCH(p, (k_heavy_fin<0, true, 2>), gh, bt, 0, st, a);
+            } else {
+                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, false, 1>), gh, bt, 0, st, a);
+                else RAE_LAUNCH(p, (k_heavy_fin<0, false, 2>), gh, bt, 0, st, a);
+            }
+        } else {
+            if (p->v4) {
+                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, true, 1>), gh, bt, 0, st, a);
+                else RAE_LAUNCH(p, (k_heavy_fin<1, true, 2>), gh, bt, 0, st, a);
+            } else {
+                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, false, 1>), gh, bt, 0, st, a);
+                else RAE_LAUNCH(p, (k_heavy_fin<1, false, 2>), gh, bt, 0, st, a);
+            }
+        }
+        HIPCHK(hipGetLastError());
+    }
     if (a.reg_on) {
         if (a.opt == RAE_OPT_ADAGRAD)
             RAE_LAUNCH(p, (k_dense_w<0>), dim3(p->grid_dense), bt, 0, st, a);

@@ -315,24 +315,95 @@ __device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bo
 //                   light A, light W (the order the update used to derive from the header)
 //   thdr[slot]      (wave tasks, workgroup tasks, 0, 0)
 // W rows are stored as ~row (negative), A rows as row.
+// exclusive block-wide prefix sum of one int per thread (fixed order), and the block total
+template <int BT>
+__device__ __forceinline__ int block_int_scan(int v, int* ws, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < BT / 64; ++i) {
+        const int c = ws[i];
+        off += (i < w) ? c : 0;
+        tot += c;
+    }
+    *total = tot;
+    return off + incl - v;
+}
+
 template <int BT>
 __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
+    __shared__ int sws[BT / 64];
     const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];
     const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
     const int HA = hA.z, HW = hW.z, LA = hA.y - hA.z, VA = hA.w, VW = hW.w;
-    const int NV = min(VA + VW, a.NVC), XV = VA + VW - NV;
-    const int T = XV + hA.y + hW.y;
     int4* vt = reinterpret_cast<int4*>(a.vtask) + slot * a.NVC;
     int4* tk = reinterpret_cast<int4*>(a.task) + slot * a.TC;
     const int4* urA = reinterpret_cast<const int4*>(a.urowA) + slot * a.RA;
     const int4* urW = reinterpret_cast<const int4*>(a.urowW) + slot * a.RW;
-    for (int v = threadIdx.x; v < VA + VW; v += BT) {
+    auto vrow = [&](int v) {
         int4 sg = v < VA ? reinterpret_cast<const int4*>(a.vrowA)[slot * a.VCA + v]
                          : reinterpret_cast<const int4*>(a.vrowW)[slot * a.VCW + v - VA];
         if (v >= VA) sg.x = ~sg.x;
-        if (v < NV) vt[v] = sg;
-        else tk[v - NV] = sg;
+        return sg;
+    };
+    // very heavy rows: rows with more than hch records become chunk tasks (the first vtask
+    // entries) plus a combine entry; the others keep one workgroup task each, overflowing to
+    // wave tasks beyond NVC
+    int NC = 0, NF = 0, NU = 0;
+    if (a.hch > 0) {
+        int4* hf = reinterpret_cast<int4*>(a.hfin) + slot * a.HF;
+        for (int v0 = 0; v0 < VA + VW; v0 += BT) {
+            const int v = v0 + threadIdx.x;
+            int4 sg = make_int4(0, 0, 0, 0);
+            int nch = 0;
+            if (v < VA + VW) {
+                sg = vrow(v);
+                const int cnt = sg.z - sg.y;
+                nch = cnt > a.hch ? (cnt + a.hch - 1) / a.hch : 0;
+            }
+            int tc, tf;
+            const int cb = NC + block_int_scan<BT>(nch, sws, &tc);
+            const int fb = NF + block_int_scan<BT>(nch > 0 ? 1 : 0, sws, &tf);
+            for (int k = 0; k < nch; ++k) {
+                const int c = cb + k;
+                if (c < a.NVC)
+                    vt[c] = make_int4(sg.x, sg.y + k * a.hch, min(sg.y + (k + 1) * a.hch, sg.z), -1 - c);
+            }
+            if (nch > 0 && fb < a.HF) hf[fb] = make_int4(sg.x, cb, nch, 0);
+            NC += tc;
+            NF += tf;
+        }
+        if (threadIdx.x == 0 && (NC > a.NVC || NF > a.HF)) atomicOr(a.err, 32);
+        NC = min(NC, a.NVC);
+        NF = min(NF, a.HF);
     }
+    for (int v0 = 0; v0 < VA + VW; v0 += BT) {        // the unchunked very heavy rows
+        const int v = v0 + threadIdx.x;
+        int4 sg = make_int4(0, 0, 0, 0);
+        bool un = false;
+        if (v < VA + VW) {
+            sg = vrow(v);
+            un = a.hch <= 0 || sg.z - sg.y <= a.hch;
+        }
+        int tu;
+        const int i = NC + NU + block_int_scan<BT>(un ? 1 : 0, sws, &tu);
+        if (un) {
+            if (i < a.NVC) vt[i] = sg;
+            else tk[i - a.NVC] = sg;
+        }
+        NU += tu;
+    }
+    const int NV = min(NC + NU, a.NVC), XV = NC + NU - NV;
+    const int T = XV + hA.y + hW.y;
     for (int t = threadIdx.x; t < T - XV; t += BT) {
         int x = t;
         int4 sg;
@@ -342,7 +413,7 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
         else { sg = urW[a.RW - 1 - (x - LA)]; sg.x = ~sg.x; }
         tk[XV + t] = sg;
     }
-    if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(T, NV, 0, 0);
+    if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(T, NV, NF, 0);
 }
 
 // Per-example descriptors of the rank's l examples of batch g (slot): everything the forward

@@ -145,6 +145,14 @@ struct StepArgs {
     // header (tasks, workgroup tasks) -- one load away from the wave that runs the task
     int32_t *thdr, *task, *vtask;
     int TC, NVC;
+    // very heavy rows with more than hch records (StepArgs::hch > 0: large global batches) are
+    // split into chunks of hch records: one workgroup task per chunk (a vtask entry whose .w is
+    // -(1 + chunk)) writes its partial gradient to hpart[chunk]; k_heavy_fin sums each row's
+    // chunks in order and applies the update -- the hfin list per slot: (row | ~row for W, first
+    // chunk, chunks, 0), thdr .z entries
+    int hch, HF, hps;    // records per chunk (0: off); combine-list capacity; floats per partial
+    float* hpart;
+    int32_t* hfin;
     // per-example descriptors of this rank's l examples per slot (rae_index.hpp):
     // [nf, p0, entity ids (NJ), feature ids (<= dcap)], dstride ints each
     int32_t* desc;

@@ -361,8 +361,9 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
     const RecBuf rb_(EXT ? a.vb : a.ex);          // the record vectors (rae_step.hpp vb)
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
-        // a one-record row's record rides in its segment: no srec round trip
-        const int rec = (en - st == 1) ? rec0 : a.srecA[base + c0 + (lane < n ? lane : 0)];
+        // a one-record row's record rides in its segment: no srec round trip (rec0 < 0: a chunk
+        // of a split row, whose records are always read from the list)
+        const int rec = (en - st == 1 && rec0 >= 0) ? rec0 : a.srecA[base + c0 + (lane < n ? lane : 0)];
         const int b = rec / NJ, j = rec - b * NJ;
         const int rb = b * a.lay.rec;
         const float* er = a.ex + rb + a.lay.ocoef + 2 * j;
@@ -449,13 +450,14 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
     const int r = a.r, nv = r / VW;
     const int64_t base = slot * a.RA;
     const int e = seg.x, st = seg.y, en = seg.z;
+    const bool chunk = seg.w < 0;                // a chunk of a split row: partial sum only
     const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
     const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
     float* prow = a.A + (int64_t)e * r;
     float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
     RowVec<V4, Q> pv, av, g;
     float ab0 = 0.f, aab0 = 0.f;
-    if (w == 0) {
+    if (w == 0 && !chunk) {
         pv.load(prow, nv, lane);
         if (OPT == 0) av.load(arow, nv, lane); else av.zero();
         ab0 = a.Ab[e];
@@ -479,6 +481,17 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
         float gt = sgb[0];
 #pragma unroll
         for (int ww = 1; ww < RAE_NWAVE; ++ww) gt += sgb[ww];
+        if (chunk) {                             // k_heavy_fin combines the row's chunks
+            typedef typename VecT<V4>::T VT;
+            float* hp = a.hpart + (int64_t)(-1 - seg.w) * a.hps;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int c = lane + RAE_WAVE * q;
+                if (c < nv) reinterpret_cast<VT*>(hp)[c] = g.v[q];
+            }
+            if (lane == 0) hp[align4(r)] = gt;
+            return;
+        }
         apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
         if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gt);
     }
@@ -498,7 +511,8 @@ __device__ __forceinline__ void feature_accum(const StepArgs& a, int64_t ex0, in
     const RecBuf rb_(a.ex);
     for (int c0 = st; c0 < en; c0 += RAE_WAVE) {
         const int n = min(RAE_WAVE, en - c0);
-        const unsigned rec = (unsigned)((en - st == 1) ? rec0 : a.srecW[base + c0 + (lane < n ? lane : 0)]);
+        const unsigned rec = (unsigned)((en - st == 1 && rec0 >= 0) ? rec0
+                                                                      : a.srecW[base + c0 + (lane < n ? lane : 0)]);
         const int b = (int)(rec >> a.posbits);
         float val = 1.f;
         if (a.values) val = a.values[a.indptr[ex0 + b] + (int)(rec & mask)];
@@ -583,10 +597,11 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
     const int m = a.m, nv = m / VW;
     const int64_t base = slot * a.RW;
     const int f = seg.x, st = seg.y, en = seg.z;
+    const bool chunk = seg.w < 0;                // a chunk of a split row: partial sum only
     const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
     const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
     RowVec<V4, Q> pv, av, g;
-    if (w == 0 && !a.reg_on) {
+    if (w == 0 && !a.reg_on && !chunk) {
         pv.load(a.W + (int64_t)f * m, nv, lane);
         if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
     }
@@ -602,7 +617,79 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
 #pragma unroll
             for (int ww = 1; ww < RAE_NWAVE; ++ww) vadd(g.v[q], spart[(ww * Q + q) * RAE_WAVE + lane]);
         }
+        if (chunk) {                             // k_heavy_fin combines the row's chunks
+            typedef typename VecT<V4>::T VT;
+            float* hp = a.hpart + (int64_t)(-1 - seg.w) * a.hps;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int c = lane + RAE_WAVE * q;
+                if (c < nv) reinterpret_cast<VT*>(hp)[c] = g.v[q];
+            }
+            return;
+        }
         feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
+    }
+}
+
+// k_heavy_fin: entry e of the slot's combine list -- a row split into chunks: the chunks'
+// partial sums in chunk order (chunk k = records [st + k hch, ...) of the row's sorted list),
+// then the update, as the unsplit row task would apply it (one wave per row)
+template <int OPT, bool V4, int Q>
+__device__ void heavy_fin(const StepArgs& a, int e, int lane) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int64_t g = step_batch(a);
+    const int64_t slot = g % a.index_window;
+    const int4 th = reinterpret_cast<const int4*>(a.thdr)[slot];
+    if (e >= th.z) return;
+    const int4 f = reinterpret_cast<const int4*>(a.hfin)[slot * a.HF + e];
+    const bool isA = f.x >= 0;
+    const int row = isA ? f.x : ~f.x;
+    const int w = isA ? a.r : a.m, nv = w / VW;
+    RowVec<V4, Q> pv, av, gs;
+    float* prow = (isA ? a.A : a.W) + (int64_t)row * w;
+    float* arow = (OPT == 0) ? (isA ? a.aA : a.aW) + (int64_t)row * w : nullptr;
+    const bool ld = isA || !a.reg_on;
+    if (ld) {
+        pv.load(prow, nv, lane);
+        if (OPT == 0) av.load(arow, nv, lane); else av.zero();
+    }
+    float ab0 = 0.f, aab0 = 0.f;
+    if (isA) {
+        ab0 = a.Ab[row];
+        aab0 = (OPT == 0) ? a.aAb[row] : 0.f;
+    }
+    gs.zero();
+    float gb = 0.f;
+    const float* hp0 = a.hpart + (int64_t)f.y * a.hps;
+    for (int k0 = 0; k0 < f.z; k0 += 8) {              // eight chunks' loads in flight
+        VT v[8][Q];
+        float b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = min(k0 + u, f.z - 1);
+            const float* hp = hp0 + (int64_t)k * a.hps;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int c = lane + RAE_WAVE * q;
+                v[u][q] = reinterpret_cast<const VT*>(hp)[c < nv ? c : 0];
+            }
+            b[u] = isA ? hp[align4(a.r)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + u < f.z) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) vadd(gs.v[q], v[u][q]);
+                gb += b[u];
+            }
+        }
+    }
+    if (isA) {
+        apply_row<OPT, V4, Q>(prow, arow, pv, av, gs, nv, a.lr, lane);
+        if (lane == 0) ab_update<OPT>(a, row, ab0, aab0, gb);
+    } else {
+        feature_finish<OPT, V4, Q>(a, row, pv, av, gs, lane);
     }
 }
 
