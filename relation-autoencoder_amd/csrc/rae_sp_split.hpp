@@ -137,7 +137,9 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
 // arithmetic as k_sp_cp: chunk c (16 deep) goes to accumulator c % 4 (k_sp_cp's wave c % 4), the
 // four summed in order -- so the split forward's own vectors and every rank's are bit-identical.
 // task = (example tile, embedding tile).
-#define RAE_VR_KC 8
+#ifndef RAE_VR_KC
+#define RAE_VR_KC 8          // 16-deep K chunks whose operand loads one round issues
+#endif
 static_assert(RAE_VR_KC % 4 == 0, "chunk u of a round feeds accumulator u % 4");
 __host__ __device__ inline int vrec_tasks(int L, int r) { return ((L + 15) / 16) * ((r + 15) / 16); }
 template <bool VEC>
