@@ -89,6 +89,7 @@ typedef struct rae_config {
     int32_t dp_update;        /* data-parallel update: RAE_DPUPD_*                          */
     int32_t priv_rows;        /* rows one record of the batch references: RAE_PRIV_*        */
     int32_t dp_dense;         /* data-parallel SP: dense decoder-matrix gradients RAE_DPDENSE_* */
+    int32_t heavy_chunk;      /* very heavy rows split into record chunks: RAE_HCHUNK_*      */
 } rae_config;
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
@@ -121,6 +122,12 @@ typedef struct rae_config {
 #define RAE_DPDENSE_PARTIALS 2 /* each rank reduces its own l examples' dC1 / dC2 / dWb before   *
                                 * the exchange (k_dpart); the records carry the partial block,  *
                                 * the update sums the ranks' blocks in rank order               */
+#define RAE_HCHUNK_AUTO 0     /* global batches of >= 2048 examples: rows with more than 128     *
+                               * records of the batch summed as 128-record chunks in parallel    *
+                               * (one partial per chunk, k_heavy_fin adds them in chunk order and *
+                               * applies the optimiser); smaller batches: off                    */
+#define RAE_HCHUNK_OFF 1      /* every very heavy row summed by one workgroup                      */
+#define RAE_HCHUNK_ON 2       /* chunks at any global batch                                        */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]

@@ -221,7 +221,7 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #define RAE_HCH 128           // very heavy rows above this many records are split into chunks
 #endif
 #ifndef RAE_HCH_MINL
-#define RAE_HCH_MINL 256      // ... in plans with a global batch of at least this many examples
+#define RAE_HCH_MINL 2048     // ... in plans with a global batch of at least this many examples
 #endif
 #ifndef RAE_NVC_MIN
 #define RAE_NVC_MIN 32
@@ -660,9 +660,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.bil_prep < RAE_BILPREP_AUTO || c.bil_prep > RAE_BILPREP_KERNEL ||
         c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED ||
         c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_OFF ||
-        c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS)
+        c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS ||
+        c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
-                                   "priv_rows / dp_dense)");
+                                   "priv_rows / dp_dense / heavy_chunk)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -821,7 +822,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
         // large global batches: very heavy rows with more than RAE_HCH records split into
         // chunks (every chunk a workgroup task: they need NVC >= all chunks of a batch)
-        a.hch = L >= RAE_HCH_MINL ? RAE_HCH : 0;
+        a.hch = (c.heavy_chunk == RAE_HCHUNK_ON ||
+                 (c.heavy_chunk == RAE_HCHUNK_AUTO && L >= RAE_HCH_MINL)) ? RAE_HCH : 0;
         if (a.hch) {
             a.HF = (a.RA + a.RW) / a.hch + 1;
             if (a.NVC < a.HF + 1) a.NVC = a.HF + 1;
@@ -1026,6 +1028,7 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
     out->priv_rows = p->args.priv ? RAE_PRIV_AUTO : RAE_PRIV_OFF;
     out->dp_dense = p->args.lay.wire == 2 ? RAE_DPDENSE_PARTIALS
                   : (p->args.lay.wire == 1 ? RAE_DPDENSE_RECORDS : 0);
+    out->heavy_chunk = p->args.hch ? RAE_HCHUNK_ON : RAE_HCHUNK_OFF;
     return RAE_OK;
 }
 

@@ -91,6 +91,7 @@ class RaeConfig(C.Structure):
         ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
         ("sp_forward", C.c_int32), ("bil_dp", C.c_int32), ("bil_prep", C.c_int32),
         ("dp_update", C.c_int32), ("priv_rows", C.c_int32), ("dp_dense", C.c_int32),
+        ("heavy_chunk", C.c_int32),
     ]
 
 
@@ -102,6 +103,7 @@ KERNEL_FORMS = {
     "dp_update": {"replicated": 0, "partitioned": 1},
     "priv_rows": {"auto": 0, "off": 1},
     "dp_dense": {"auto": 0, "records": 1, "partials": 2},
+    "heavy_chunk": {"auto": 0, "off": 1, "on": 2},
 }
 
 

@@ -194,9 +194,10 @@ class TrainEngine:
         ca, cw = self._dp_caps or (0, 0)
         if self._dp_send is not None and need_a <= ca and need_w <= cw:
             return
-        # headroom: later windows' lists vary by a few percent around the first's
-        ca = min(max(ca, int(need_a * 1.25) + 16), self._dp_cap_max[0])
-        cw = min(max(cw, int(need_w * 1.25) + 16), self._dp_cap_max[1])
+        # headroom: the first window's longest list is already the tail of many batches, and
+        # a longer one later only re-sizes (a one-off): every padded row travels every step
+        ca = min(max(ca, int(need_a * 1.04) + 16), self._dp_cap_max[0])
+        cw = min(max(cw, int(need_w * 1.04) + 16), self._dp_cap_max[1])
         blk = int(self.lib.rae_dp_block_floats(C.byref(self.cfg), ca, cw))
         self._dp_send = torch.zeros(self.world_size * blk, dtype=torch.float32, device=self.device)
         self._dp_recv = torch.zeros_like(self._dp_send)
@@ -255,7 +256,8 @@ class TrainEngine:
         does), dp_update replicated|partitioned, priv_rows auto|off (rows one record of the
         batch references updated per example, or by the row tasks), dp_dense records|partials
         (data-parallel SP: dw1 / dw2 per example in the exchange, or each rank's reduced dense
-        gradients).  Keys of forms that do not apply to the plan are left out."""
+        gradients), heavy_chunk off|on (rows with more than 128 records of the global batch
+        summed as parallel 128-record chunks).  Keys of forms that do not apply to the plan are left out."""
         out = _lib.RaeConfig()
         _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
         F = _lib.KERNEL_FORMS
@@ -272,6 +274,7 @@ class TrainEngine:
         res["priv_rows"] = name["priv_rows"][out.priv_rows]
         if sp and self.world_size > 1:
             res["dp_dense"] = name["dp_dense"][out.dp_dense]
+        res["heavy_chunk"] = name["heavy_chunk"][out.heavy_chunk]
         return res
 
     def _moves(self):

@@ -206,7 +206,7 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto"):
              costs=np.concatenate(ind.epoch_costs), **params)
 
 
-def run_gpu_c3(out, steps=3, dp_update="replicated"):
+def run_gpu_c3(out, steps=3, dp_update="replicated", heavy_chunk="auto"):
     """BASELINE config 3 at full size (1M triples) with the global batch of 8 ranks at l=100,
     L = 800, split over 2 ranks of l = 400: the first `steps` batches of an epoch, negatives
     from the reference's RandomState stream (device CDF search)."""
@@ -221,8 +221,10 @@ def run_gpu_c3(out, steps=3, dp_update="replicated"):
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 800 // ws, 200, 100,
                              20, 0.0, 0.0, "adagrad", "dp800", "sp", False, True, False, 1.0,
                              device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
-                             dp_update=dp_update)
+                             dp_update=dp_update, kernel_forms={"heavy_chunk": heavy_chunk})
     ind.compile_function()
+    if heavy_chunk != "auto":
+        assert ind.engine.kernel_forms_in_use()["heavy_chunk"] == heavy_chunk
     eng = ind.engine
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
     eng.run(0, steps)
@@ -354,7 +356,8 @@ def main():
             run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated",
                     sys.argv[5] if len(sys.argv) > 5 else "auto")
         elif mode == "gpu_c3":
-            run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated")
+            run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
+                       heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")
         elif mode == "gpu_ckpt":
             run_gpu_ckpt(out, dec)
         elif mode == "nccl1":

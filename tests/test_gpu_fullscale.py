@@ -67,7 +67,8 @@ def check_labels(got, xs, W, Wb, margin=LABEL_MARGIN, what="", W_gpu=None, Wb_gp
     return float(decisive.mean())
 
 
-def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234, labels=False):
+def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234, labels=False,
+         kernel_forms=None):
     import torch
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
@@ -83,9 +84,11 @@ def _run(cuda_dev, N, d, m, r, s, l, ntrue, steps, seed_data=1234, labels=False)
 
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
                              "adagrad", "fullscale", "sp", False, True, False, 1.0,
-                             device=cuda_dev, graph_chunk=2)
+                             device=cuda_dev, graph_chunk=2, kernel_forms=kernel_forms)
     ind.compile_function()
     eng = ind.engine
+    for k, v in (kernel_forms or {}).items():
+        assert eng.kernel_forms_in_use()[k] == v
     eng.set_epoch_negatives(neg1, neg2)
     eng.run(0, steps)
     torch.cuda.synchronize()
@@ -248,12 +251,15 @@ def test_c4_shape(built_lib, cuda_dev):
     _check(want_c, got_c, want_p, got_p, init)
 
 
-def test_c3_global_batch_800(built_lib, cuda_dev):
+@pytest.mark.parametrize("heavy_chunk", ["off", "on"])
+def test_c3_global_batch_800(built_lib, cuda_dev, heavy_chunk):
     # the global batch of 8 data-parallel ranks at l = 100: Zipf-frequent rows carry hundreds
-    # of records per step (workgroup rows split over four waves) and every K-chunk of the
-    # dense tiles is non-trivial
+    # of records per step (workgroup rows split over four waves, or -- heavy_chunk on, the
+    # default from L = 2048 -- into 128-record chunks summed in parallel and combined by
+    # k_heavy_fin) and every K-chunk of the dense tiles is non-trivial
     want_c, got_c, want_p, got_p, init = _run(cuda_dev, N=1_000_000, d=2 ** 17, m=100, r=200,
-                                              s=20, l=800, ntrue=100, steps=3)
+                                              s=20, l=800, ntrue=100, steps=3,
+                                              kernel_forms={"heavy_chunk": heavy_chunk})
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
 
 
@@ -357,15 +363,16 @@ def test_c4_full_size(built_lib, cuda_dev):
     assert np.array_equal(named["A"][ue_t].cpu().numpy(), A0)
 
 
-@pytest.mark.parametrize("dp_update", ["replicated", "partitioned"])
-def test_c3_global_batch_800_two_ranks(built_lib, cuda_dev, tmp_path, dp_update):
+@pytest.mark.parametrize("dp_update,heavy_chunk", [("replicated", "auto"), ("partitioned", "auto"),
+                                                   ("partitioned", "on")])
+def test_c3_global_batch_800_two_ranks(built_lib, cuda_dev, tmp_path, dp_update, heavy_chunk):
     """The data-parallel path itself at C3's full size: 2 ranks x l = 400 (the global batch of
     8 ranks at l = 100), records all-gathered between the forward and the update (replicated:
     every rank updates every row; partitioned: each rank its own rows, rows pulled from their
     owners before each forward), against the float64 oracle at the global batch L = 800; the
     two replicas bit-identical (partitioned: after the final gather)."""
     import test_dist
-    test_dist._launch(["gpu_c3", str(tmp_path), dp_update], timeout=600)
+    test_dist._launch(["gpu_c3", str(tmp_path), dp_update, heavy_chunk], timeout=600)
     want_c, _, want_p, _, init = _run_oracle_only(N=1_000_000, d=2 ** 17, m=100, r=200, s=20,
                                                   l=800, ntrue=100, steps=3)
     c0 = np.load(tmp_path / "c3_costs_0.npy").astype(np.float64)

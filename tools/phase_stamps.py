@@ -6,7 +6,11 @@ prints, for k_forward, the median/max duration of each phase per workgroup kind 
 dispatch skew, and for k_update the per-task-type durations.  Diagnostic only: stamps add
 barriers' worth of serialisation, so read shares, not absolute kernel time.
 
-    python tools/phase_stamps.py [--config c3] [--iters 10]
+    python tools/phase_stamps.py [--config c3] [--iters 10] [--batch-size 100]
+                                 [--G 8 --dp-update replicated|partitioned]
+
+With --G > 1 the plan is rank 0 of a G-rank data-parallel plan whose collectives are no-ops
+(tools/probes/dp_update_model.py's NoPeers): the update then runs over the global batch G*l.
 """
 import argparse
 import ctypes as C
@@ -42,6 +46,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=100)
+    ap.add_argument("--G", type=int, default=1)
+    ap.add_argument("--dp-update", default="replicated")
     args = ap.parse_args()
     build_diag()
     os.environ["RAE_LIB"] = DIAG
@@ -55,10 +61,16 @@ def main():
     lib.rae_debug_grid.argtypes = [C.c_void_p, C.c_void_p]
     cfg = bench.CONFIGS[args.config]
     dev = torch.device("cuda", 0)
+    dp = {}
+    if args.G > 1:
+        sys.path.insert(0, os.path.join(ROOT, "tools", "probes"))
+        from dp_update_model import NoPeers
+        dp = dict(world_size=args.G, rank=0, exchange=NoPeers(args.G), dp_update=args.dp_update)
     data, gold = synthetic_dataset(cfg["N"], cfg["d"], cfg["ntrue"], seed=1234)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.batch_size,
                              cfg["r"], cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "stamps",
-                             cfg["dec"], False, True, False, 1.0, device=dev, graph_chunk=1)
+                             cfg["dec"], False, True, False, 1.0, device=dev, graph_chunk=1,
+                             **dp)
     ind.compile_function()
     eng = ind.engine
     n1, n2 = ind.draw_epoch_negatives()

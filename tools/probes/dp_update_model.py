@@ -133,7 +133,9 @@ def project(res, args):
         r = res.get(mode)
         if not r:
             continue
-        tg = r["index_per_batch"] + r["forward"] + r["update"] + coll(r["records_allgather_in_bytes"])
+        tg = r["index_per_batch"] + r["forward"] + r["update"]
+        if "records_allgather_in_bytes" in r:
+            tg += coll(r["records_allgather_in_bytes"])
         if "pack" in r:
             tg += r["pack"] + r["unpack"] + coll(r["rows_alltoall_in_bytes"])
         proj[mode] = {"step_us": tg, "efficiency": t1 / tg}
