@@ -174,6 +174,18 @@ __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, const D& Dm, 
     }
 }
 
+// diagnostic knockouts of the C3 forward's data movement (variant builds only, wrong results:
+// timing of the chain without the decoder-matrix ingest / W-row gather / A-row gather)
+#ifndef RAE_KO_C
+#define RAE_KO_C 0
+#endif
+#ifndef RAE_KO_W
+#define RAE_KO_W 0
+#endif
+#ifndef RAE_KO_A
+#define RAE_KO_A 0
+#endif
+
 // ---- decoder weight matrices C1, C2 (r, m) in registers ----------------------------------
 // group gid (16 lanes) owns rows i = gid + NG*ra, lane q owns column vectors c = q + 16*cc.
 // Fixed shapes that fit keep the whole pair resident for both matvecs; otherwise the
@@ -198,7 +210,11 @@ struct CCache {
         const int gid = threadIdx.x >> 4, q = threadIdx.x & 15;
 #pragma unroll
         for (int ra = 0; ra < RA; ++ra) {
+#if RAE_KO_C     // diagnostic knockout (wrong results): every lane reads row 0 (L1-hot C)
+            const int i = 0;
+#else
             const int i = min(r0 + gid + RAE_NG * ra, Dm.r - 1);
+#endif
 #pragma unroll
             for (int cc = 0; cc < CC; ++cc) {
                 const int c = min(c0 + q + 16 * cc, mv - 1);
@@ -836,7 +852,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         for (int k = 0; k < KF; ++k) {
             const int f = slot + NSL * k;
             const bool ok = slot < NSL && f < nf;
-            const int fi = S.sfidx[f < 256 ? f : 255];
+            const int fi = RAE_KO_W ? 0 : S.sfidx[f < 256 ? f : 255];   // knockout: row 0
             wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
             fv[k] = ok ? S.sfval[f < 256 ? f : 255] : 0.f;
         }
@@ -862,7 +878,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
             const int rho = (w - 4) + 4 * k;
             if (rho < NR && lane < r / 4) {
                 const int j = rho == 0 ? 0 : rho + 1;            // SP: e2's row is not read
-                const float* src = a.A + (int64_t)S.sids[j] * r + (int64_t)ln * 4;
+                const float* src = a.A + (int64_t)(RAE_KO_A ? 0 : S.sids[j]) * r + (int64_t)ln * 4;
                 dma_row16(src, lds_addr(arows + rho * r4));
             }
         }
