@@ -69,7 +69,7 @@ class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
                  index_window=0, device=None, mfma_bf16=False, kernel_forms=None,
-                 graph_absolute=False, dp_update="replicated"):
+                 graph_absolute=False, dp_update="replicated", index_overlap=True):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -181,6 +181,16 @@ class TrainEngine:
         # run() then sets the cursor again (cursor_moved() forces the same).
         self._cursor_at = None
         self._moves_seen = self._moves()
+        # index_overlap: run() builds the next window's row index on a lowest-priority side
+        # stream while the current window's steps run (the index is parameter independent; a
+        # batch's slot is batch % index_window, so windows of half the ring never touch the
+        # slots the steps in flight read).  Otherwise each window is built on the step stream
+        # right before its steps.
+        self.index_overlap = bool(index_overlap) and self.index_window >= 2
+        self._win = self.index_window // 2 if self.index_overlap else self.index_window
+        self._idx_stream = None
+        self._ready = None           # (lo, hi, negatives version, side-stream event): _mark_built
+        self._neg_version = 0
 
     # ------------------------------------------------------------------ partitioned update
     def _dp_caps_check(self):
@@ -237,6 +247,10 @@ class TrainEngine:
 
     def close(self):
         if getattr(self, "plan", None):
+            rd = getattr(self, "_ready", None)
+            if rd is not None and rd[3] is not None:
+                rd[3].synchronize()
+            self._ready = None
             self._graphs.clear()
             self.lib.rae_plan_destroy(self.plan)
             self.plan = None
@@ -307,6 +321,7 @@ class TrainEngine:
         b = int(batch_index)
         if not 0 <= b < self.nb:
             raise IndexError(f"batch index {b} out of range [0, {self.nb})")
+        self._new_negatives()            # its index slot is rebuilt with the call's negatives
         self.call_neg[0].copy_(torch.from_numpy(n1))
         self.call_neg[1].copy_(torch.from_numpy(n2))
         st = self._stream()
@@ -321,6 +336,7 @@ class TrainEngine:
     # ------------------------------------------------------------------ epoch path
     def set_epoch_negatives(self, neg1, neg2):
         """(s, N) negatives of one epoch (OieInduction.py:183-184), host or device."""
+        self._new_negatives()
         self.neg1.copy_(torch.as_tensor(np.asarray(neg1, dtype=np.int32)) if not
                         torch.is_tensor(neg1) else neg1)
         self.neg2.copy_(torch.as_tensor(np.asarray(neg2, dtype=np.int32)) if not
@@ -336,6 +352,7 @@ class TrainEngine:
         mode "philox": uniforms generated on the device (rae_neg_sample_philox, counter =
           (epoch, buffer, draw)) -- no host work at all, not the reference's stream."""
         count = self.N * self.s
+        self._new_negatives()
         if getattr(self, "_cum_dev", None) is None:
             self._cum_dev = torch.as_tensor(np.asarray(sampler.cum, dtype=np.float64),
                                             device=self.device)
@@ -446,10 +463,11 @@ class TrainEngine:
         self._graph(int(count or self.graph_chunk))
 
     def windows(self, first_batch: int, count: int):
-        """The index windows run() walks: [(first batch, batches), ...]."""
+        """The index windows run() walks: [(first batch, batches), ...] (half the ring each
+        with index_overlap)."""
         out, b, end = [], int(first_batch), int(first_batch) + int(count)
         while b < end:
-            n = min(self.index_window, end - b)
+            n = min(self._win, end - b)
             out.append((b, n))
             b += n
         return out
@@ -481,8 +499,10 @@ class TrainEngine:
 
     def build_index(self, first_batch: int, count: int):
         """Row index of batches [first_batch, first_batch+count) (one window at most)."""
+        self._drain_prefetch()
         _lib.check(self.lib.rae_build_index(self.plan, int(first_batch), int(count), self._stream()),
                    "rae_build_index")
+        self._mark_built(int(first_batch), int(first_batch) + int(count))
         if self._dp:
             self._dp_caps_check()
 
@@ -498,13 +518,17 @@ class TrainEngine:
         if self._dp:
             self._stale.update(("params", "acc"))
         replays = self._cursor_replays(first_batch, count, last_advance)
-        for wi, (b, n) in enumerate(self.windows(first_batch, count)):
+        wins = self.windows(first_batch, count)
+        for wi, (b, n) in enumerate(wins):
             if index:
-                _lib.check(self.lib.rae_build_index(self.plan, b, n, self._stream()),
-                           "rae_build_index")
-                self.check()
-                if self._dp:
-                    self._dp_caps_check()
+                self._index_ready(b, n)
+                if self.index_overlap:
+                    # the next window (of this run, or the one a following run starts with):
+                    # built beside this window's steps
+                    nb_ = wins[wi + 1][0] if wi + 1 < len(wins) else b + n
+                    nn_ = wins[wi + 1][1] if wi + 1 < len(wins) else min(self._win, self.nb - nb_)
+                    if nn_ > 0:
+                        self.prefetch_index(nb_, nn_)
             if graph and self.graph_chunk > 1 and self.graph_absolute:
                 for cb, cn in self._chunks(b, n):
                     self._graph(cn, cb).replay()
@@ -521,6 +545,74 @@ class TrainEngine:
                     self._graph(cnt, advance=adv).replay()
                 self._cursor_at = b + n - (0 if reps[-1][1] else reps[-1][0])
             self._moves_seen = self._moves()
+
+    # ------------------------------------------------------------------ index overlap
+    # self._ready = (lo, hi, negatives version, event): batches [lo, hi) have their row index
+    # in the ring; event (or None) marks the end of a side-stream build not yet waited for.
+    def _mark_built(self, x: int, y: int, event=None):
+        lo, hi, ver, ev = self._ready if self._ready else (x, x, self._neg_version, None)
+        if ver != self._neg_version or x != hi:      # not contiguous: a new range
+            lo, ev = x, None
+        self._ready = (max(lo, y - self.index_window), y, self._neg_version, event or ev)
+
+    def _covered(self, b: int, e: int) -> bool:
+        rd = self._ready
+        return rd is not None and rd[2] == self._neg_version and rd[0] <= b and e <= rd[1]
+
+    def prefetch_index(self, first_batch: int, count: int):
+        """Start the row index of batches [first_batch, first_batch+count) -- the part not
+        already built -- on the side stream, behind everything queued on the step stream so
+        far, in front of whatever is queued after.  Steps queued after it may read batches
+        >= first_batch + count - index_window only (a window of half the ring ahead of the
+        window being run satisfies that)."""
+        if not self.index_overlap:
+            raise RuntimeError("prefetch_index needs index_overlap")
+        x, y = int(first_batch), int(first_batch) + int(count)
+        rd = self._ready
+        if rd is not None and rd[2] == self._neg_version and rd[0] <= x <= rd[1]:
+            x = max(x, rd[1])                        # extend the built range
+        if y <= x:
+            return
+        if self._idx_stream is None:
+            lo, _ = torch.cuda.Stream.priority_range()
+            self._idx_stream = torch.cuda.Stream(self.device, priority=lo)
+        self._idx_stream.wait_stream(torch.cuda.current_stream(self.device))
+        _lib.check(self.lib.rae_build_index(self.plan, x, y - x,
+                                            C.c_void_p(self._idx_stream.cuda_stream)),
+                   "rae_build_index")
+        done = torch.cuda.Event()
+        done.record(self._idx_stream)
+        self._mark_built(x, y, done)
+
+    def _index_ready(self, b: int, n: int):
+        """The window [b, b+n)'s index before its steps: already in the ring (a side-stream
+        build the step stream then waits for), else built on the step stream; then the
+        overflow check (host sync) and, partitioned, the row-list capacities."""
+        if self._covered(b, b + n):
+            ev = self._ready[3]
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                ev.synchronize()
+                self._ready = self._ready[:3] + (None,)
+        else:
+            self._drain_prefetch()
+            _lib.check(self.lib.rae_build_index(self.plan, b, n, self._stream()),
+                       "rae_build_index")
+            self._mark_built(b, b + n)
+        self.check()
+        if self._dp:
+            self._dp_caps_check()
+
+    def _drain_prefetch(self):
+        """A side-stream build still in flight: the step stream waits for it (it uses the
+        plan's index scratch and reads the negatives)."""
+        if self._ready is not None and self._ready[3] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._ready[3])
+            self._ready = self._ready[:3] + (None,)
+
+    def _new_negatives(self):
+        self._drain_prefetch()
+        self._neg_version += 1
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):

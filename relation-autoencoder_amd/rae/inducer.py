@@ -54,7 +54,8 @@ class ReconstructInducer:
                  model_name, decoder_model, external_embeddings, extended_regularizer,
                  frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
                  graph_chunk=64, neg_sampler="device", neg_seed=0, mfma_bf16=False,
-                 kernel_forms=None, dp_update="replicated"):
+                 kernel_forms=None, dp_update="replicated", index_window=0,
+                 index_overlap=True):
         self.data = data
         self.goldStandard = gold_standard
         self.rng = rng
@@ -84,6 +85,8 @@ class ReconstructInducer:
         self.neg_seed = int(neg_seed)
         self.mfma_bf16 = bool(mfma_bf16)   # RESCAL / hybrid: bf16 MFMA operands (config 5)
         self.kernel_forms = dict(kernel_forms or {})   # engine.TrainEngine kernel_forms
+        self.index_window = int(index_window)          # engine.TrainEngine row-index ring
+        self.index_overlap = bool(index_overlap)
         self.dp_update = dp_update         # "replicated" | "partitioned" (rae/dist.py)
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
@@ -148,7 +151,8 @@ class ReconstructInducer:
                                   rank=self.rank, exchange=self.exchange,
                                   graph_chunk=self.graph_chunk, device=self.device,
                                   mfma_bf16=self.mfma_bf16, kernel_forms=self.kernel_forms,
-                                  dp_update=self.dp_update)
+                                  dp_update=self.dp_update, index_window=self.index_window,
+                                  index_overlap=self.index_overlap)
         self.func["train"] = _TrainFunction(self.engine)
         for key in self.data.generate_split_keys():
             ds = self.engine.split if key == "train" else DeviceSplit(self.data.split[key], self.device)

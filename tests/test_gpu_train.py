@@ -159,6 +159,62 @@ def test_split_sp_forward_vs_oracle(built_lib, cuda_dev, shape):
     _assert_params_close(_params(ind), tr.params, "split")
 
 
+@pytest.mark.parametrize("dec", ["sp", "rescal"])
+def test_index_overlap_matches_serial(built_lib, cuda_dev, dec):
+    """engine.run builds the next window's row index on a lowest-priority side stream while the
+    current window's steps run (index_overlap; windows of half the ring).  A ring of 8 batches
+    over two epochs (many windows, every side build behind the step stream's queue), serial
+    windows of 8, and one window per epoch train bit-identically; so does a run cut into
+    per-batch runs (frequentEval mode 2's pattern: every window already built by the last
+    run's prefetch)."""
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    out = []
+    for iw, ov in ((8, True), (8, False), (0, True)):
+        data, gold = synthetic_dataset(1500, 3000, 10, seed=31)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, 50, 24, 12, 5,
+                                 0.0, 0.0, "adagrad", "ovl", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, index_window=iw,
+                                 index_overlap=ov)
+        ind.learn(verbose=False)
+        eng = ind.engine
+        assert eng.index_overlap == ov
+        if iw:
+            assert eng.index_window == 8
+            assert len(eng.windows(0, eng.nb)) >= (6 if ov else 3)
+        out.append((_params(ind), np.array(ind.epoch_costs)))
+    # per-batch runs (eager, as frequentEval mode 2 runs them) on a fresh model
+    data, gold = synthetic_dataset(1500, 3000, 10, seed=31)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 50, 24, 12, 5,
+                             0.0, 0.0, "adagrad", "ovl1", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2, index_window=8)
+    ind.compile_function()
+    eng = ind.engine
+    n1, n2 = ind.draw_epoch_negatives()
+    eng.set_epoch_negatives(n1, n2)
+    for b in range(eng.nb):
+        eng.run(b, 1, graph=False)
+    torch.cuda.synchronize()
+    eng.check()
+    ref = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 50, 24, 12, 5,
+                             0.0, 0.0, "adagrad", "ovl2", dec, False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=2, index_overlap=False)
+    ref.compile_function()
+    n1r, n2r = ref.draw_epoch_negatives()
+    assert np.array_equal(n1, n1r)
+    ref.engine.set_epoch_negatives(n1r, n2r)
+    ref.engine.run(0, ref.engine.nb)
+    torch.cuda.synchronize()
+    for k, v in _params(ref).items():
+        assert np.array_equal(_params(ind)[k], v), f"per-batch runs: {k}"
+    for k in out[0][0]:
+        for o in out[1:]:
+            assert np.array_equal(out[0][0][k], o[0][k]), k
+    for o in out[1:]:
+        assert np.array_equal(out[0][1], o[1])
+
+
 def test_bitwise_deterministic(built_lib, cuda_dev):
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer

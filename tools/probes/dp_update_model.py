@@ -10,10 +10,15 @@ Times, per step, with the kernels' own dispatch timestamps (rae_time_next):
   replicated   rank 0 of a G-rank plan: forward (l examples), update over the global batch
                L = G*l (with the SP wire record: k_vrec + k_update), row index of the global batch;
   partitioned  the same with the row-owner partitioned update: + the row pull's pack / unpack.
+Whole steps as the epoch loop runs them (graph replays of n steps, HIP events): alone
+("graph_step") and with the next n batches' row index built beside them on the side stream
+("graph_step_with_index": engine index_overlap).
 Bytes: the records all-gather and the rows all-to-all inbound per rank per step.  The
-projection puts each collective at  lat_us + inbound bytes / (links * link_gbs * eff)  on the
-step's critical path (no overlap with the kernels) and reports the weak-scaling efficiency
-t_single / t_G.  DESIGN.md sec. 4 holds the table of one run."""
+projection takes graph_step_with_index (kernels, launch gaps and the overlapped index, the
+no-op collectives' slots empty) and adds each collective at
+lat_us + inbound bytes / (links * link_gbs * eff)  (no overlap with the kernels); it reports
+the weak-scaling efficiency t_single / t_G, t_single the same measure of the G = 1 plan.
+DESIGN.md sec. 4 holds the table of one run."""
 import argparse
 import ctypes as C
 import json
@@ -51,7 +56,7 @@ def measure(args, cfg, data, gold, G, mode):
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
                              cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
                              True, False, 1.0, device=dev, world_size=G, rank=0,
-                             exchange=NoPeers(G) if G > 1 else None, graph_chunk=1,
+                             exchange=NoPeers(G) if G > 1 else None, graph_chunk=args.graph_n,
                              mfma_bf16=cfg.get("bf16", False), dp_update=mode,
                              kernel_forms=dict(kv.split("=", 1) for kv in args.kernel_form)
                              if G > 1 else None)
@@ -113,32 +118,68 @@ def measure(args, cfg, data, gold, G, mode):
         out["rows_alltoall_in_bytes"] = (G - 1) * blk
         out["row_caps"] = [ca, cw]
     out["kernel_forms"] = eng.kernel_forms_in_use()
+    out.update(graph_steps(eng, args))
     ind._drop_engine()
     return out
+
+
+def graph_steps(eng, args):
+    """us per step of n graph-replayed steps, alone and with the next n batches' index built
+    beside them (prefetch_index on the side stream), medians over reps."""
+    import torch
+    n = min(args.graph_n, eng.index_window // 2, eng.nb // 2)
+    eng.cursor_moved()
+    eng.build_index(0, n)
+    eng.capture_for(0, n)
+    eng.run(0, n, index=False)
+    main = torch.cuda.current_stream()
+    alone, ovl = [], []
+    for _ in range(args.reps):
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(main)
+        eng.run(0, n, index=False)
+        b.record(main)
+        torch.cuda.synchronize()
+        alone.append(a.elapsed_time(b) * 1e3 / n)
+        eng._ready = None                   # force the rebuild of [n, 2n) each rep
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(main)
+        eng.prefetch_index(n, n)
+        eng.run(0, n, index=False)
+        main.wait_event(eng._ready[3])
+        b.record(main)
+        torch.cuda.synchronize()
+        ovl.append(a.elapsed_time(b) * 1e3 / n)
+    return {"graph_steps_n": n, "graph_step": float(np.median(alone)),
+            "graph_step_with_index": float(np.median(ovl))}
 
 
 def project(res, args):
     bw = args.links * args.link_gbs * args.eff * 1e3          # bytes per us
     coll = lambda b: args.lat_us + b / bw                      # noqa: E731
     s = res["single"]
-    t1 = s["forward"] + s["update"] + s["index_per_batch"]
+    t1 = s["graph_step_with_index"]
     proj = {"single_step_us": t1,
             "assumptions": {"link_gbs_per_direction": args.link_gbs, "links": args.links,
                             "efficiency": args.eff, "collective_latency_us": args.lat_us,
                             "inbound_GBs": bw / 1e3,
-                            "model": "step = index + [pack + A2A + unpack] + forward + AG + "
-                                     "update, every collective lat + bytes / inbound rate, "
-                                     "nothing overlapped"}}
+                            "model": "step = graph-replayed step with the index built beside "
+                                     "it (measured) + A2A (partitioned) + AG, every collective "
+                                     "lat + bytes / inbound rate, not overlapped"}}
     for mode in ("replicated", "partitioned"):
         r = res.get(mode)
         if not r:
             continue
-        tg = r["index_per_batch"] + r["forward"] + r["update"]
+        tg = r["graph_step_with_index"]
+        comm = 0.0
         if "records_allgather_in_bytes" in r:
-            tg += coll(r["records_allgather_in_bytes"])
-        if "pack" in r:
-            tg += r["pack"] + r["unpack"] + coll(r["rows_alltoall_in_bytes"])
-        proj[mode] = {"step_us": tg, "efficiency": t1 / tg}
+            comm += coll(r["records_allgather_in_bytes"])
+        if "rows_alltoall_in_bytes" in r:
+            comm += coll(r["rows_alltoall_in_bytes"])
+        proj[mode] = {"step_us": tg + comm, "kernels_us": tg, "collectives_us": comm,
+                      "efficiency": t1 / (tg + comm),
+                      "efficiency_if_collectives_free": t1 / tg}
     return proj
 
 
@@ -150,6 +191,8 @@ def main():
     ap.add_argument("--l", type=int, default=100)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--graph-n", type=int, default=64, help="steps per timed graph replay")
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="replicated,partitioned")
     ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
                     help="kernel form of the G-rank plans (e.g. priv_rows=off)")
