@@ -313,15 +313,14 @@ def main():
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # the index of the batches after the timed ones, built beside them as the epoch loop
-    # overlaps a window's build with the previous window's steps (engine.prefetch_index)
+    # the index of the K batches after the timed ones, built beside them in slices as the
+    # epoch loop builds a window's successor (engine.run prefetch)
     npref = 0
-    if prebuilt and eng.index_overlap:
-        npref = max(0, min(K, eng.windows(0, eng.nb)[0][1], eng.index_window - K, nb - W - K))
-        if npref:
-            eng.prefetch_index(W + K, npref)
+    if prebuilt and eng.index_overlap and 2 * K <= eng.index_window:
+        npref = max(0, min(K, nb - W - K))
     # no run follows the timed one on this cursor: its last graph skips the cursor advance
-    eng.run(W, K, index=not prebuilt, last_advance=False)
+    eng.run(W, K, index=not prebuilt, last_advance=False,
+            prefetch=None if not prebuilt else npref > 0)
     t_host = time.perf_counter() - t0          # host time to queue the timed region's work
     torch.cuda.synchronize()
     rdist.barrier()

@@ -189,6 +189,9 @@ class TrainEngine:
         self.index_overlap = bool(index_overlap) and self.index_window >= 2
         self._win = self.index_window // 2 if self.index_overlap else self.index_window
         self._idx_stream = None
+        if self.index_overlap:
+            lo, _ = torch.cuda.Stream.priority_range()
+            self._idx_stream = torch.cuda.Stream(self.device, priority=lo)
         self._ready = None           # (lo, hi, negatives version, side-stream event): _mark_built
         self._neg_version = 0
 
@@ -507,44 +510,69 @@ class TrainEngine:
             self._dp_caps_check()
 
     def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True,
-            last_advance: bool = True):
+            last_advance: bool = True, prefetch: bool | None = None):
         """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
         negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
-        of each window of batches is built right before the window's steps (index=False:
-        the caller built it already, e.g. bench.py ahead of its timed region).  With graph,
-        every step runs inside a replayed HIP graph: graph_chunk-step graphs and one graph
-        per window remainder (last_advance: see _cursor_replays)."""
+        of each window of batches is ready before the window's steps (index=False: the caller
+        built it already, e.g. bench.py ahead of its timed region).  With index_overlap and
+        prefetch (default: index), the index of the batches after each window -- the run's
+        next window, or as many batches as the window after the run's last -- is built on the
+        side stream in slices, one in front of each graph replay (or graph_chunk eager steps),
+        so each slice runs beside the steps queued after it; one whole-window build beside
+        the steps slows them for its whole duration instead (measured: bench.py C3 17.4 ->
+        28 us/step).  With graph, every step runs inside a replayed HIP graph:
+        graph_chunk-step graphs and one graph per window remainder (last_advance: see
+        _cursor_replays)."""
         self._ensure_epoch_mode()
         if self._dp:
             self._stale.update(("params", "acc"))
+        pre = (index if prefetch is None else prefetch) and self.index_overlap
         replays = self._cursor_replays(first_batch, count, last_advance)
         wins = self.windows(first_batch, count)
+        st = self._stream()
         for wi, (b, n) in enumerate(wins):
             if index:
                 self._index_ready(b, n)
-                if self.index_overlap:
-                    # the next window (of this run, or the one a following run starts with):
-                    # built beside this window's steps
-                    nb_ = wins[wi + 1][0] if wi + 1 < len(wins) else b + n
-                    nn_ = wins[wi + 1][1] if wi + 1 < len(wins) else min(self._win, self.nb - nb_)
-                    if nn_ > 0:
-                        self.prefetch_index(nb_, nn_)
+            nxt = None
+            if pre:
+                nn_ = wins[wi + 1][1] if wi + 1 < len(wins) else min(n, self.nb - (b + n))
+                nxt = (b + n, nn_) if nn_ > 0 else None
             if graph and self.graph_chunk > 1 and self.graph_absolute:
-                for cb, cn in self._chunks(b, n):
-                    self._graph(cn, cb).replay()
+                chunks = [(lambda cb=cb, cn=cn: self._graph(cn, cb).replay())
+                          for cb, cn in self._chunks(b, n)]
+                for go, sl in zip(chunks, self._slices(nxt, len(chunks))):
+                    if sl:
+                        self.prefetch_index(*sl)
+                    go()
                 continue
             if self._cursor_at != b or self._moves_seen != self._moves():
                 self.set_cursor(b)
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
-                self._steps_eager(n, self._stream())
-                self._cursor_at = b + n
+                piece = self.graph_chunk if self.graph_chunk > 1 else 64
+                chunks = [(lambda c=min(piece, n - k): self._steps_eager(c, st))
+                          for k in range(0, n, piece)]
+                at = b + n
             else:
                 reps = replays[wi]
-                for cnt, adv in reps:
-                    self._graph(cnt, advance=adv).replay()
-                self._cursor_at = b + n - (0 if reps[-1][1] else reps[-1][0])
+                chunks = [(lambda c=cnt, a=adv: self._graph(c, advance=a).replay())
+                          for cnt, adv in reps]
+                at = b + n - (0 if reps[-1][1] else reps[-1][0])
+            for go, sl in zip(chunks, self._slices(nxt, len(chunks))):
+                if sl:
+                    self.prefetch_index(*sl)
+                go()
+            self._cursor_at = at
             self._moves_seen = self._moves()
+
+    @staticmethod
+    def _slices(nxt, k):
+        """[first, count) split into k consecutive slices (None where nothing is left)."""
+        if nxt is None:
+            return [None] * k
+        b, n = nxt
+        q = -(-n // k)
+        return [(b + i * q, min(q, n - i * q)) if i * q < n else None for i in range(k)]
 
     # ------------------------------------------------------------------ index overlap
     # self._ready = (lo, hi, negatives version, event): batches [lo, hi) have their row index
@@ -573,9 +601,6 @@ class TrainEngine:
             x = max(x, rd[1])                        # extend the built range
         if y <= x:
             return
-        if self._idx_stream is None:
-            lo, _ = torch.cuda.Stream.priority_range()
-            self._idx_stream = torch.cuda.Stream(self.device, priority=lo)
         self._idx_stream.wait_stream(torch.cuda.current_stream(self.device))
         _lib.check(self.lib.rae_build_index(self.plan, x, y - x,
                                             C.c_void_p(self._idx_stream.cuda_stream)),
