@@ -313,8 +313,8 @@ def main():
     rdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # the index of the K batches after the timed ones, built beside them in slices as the
-    # epoch loop builds a window's successor (engine.run prefetch)
+    # the index of the K batches after the timed ones, built beside them as the epoch loop
+    # builds a window's successor (engine.run prefetch)
     npref = 0
     if prebuilt and eng.index_overlap and 2 * K <= eng.index_window:
         npref = max(0, min(K, nb - W - K))

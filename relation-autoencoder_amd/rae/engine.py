@@ -192,6 +192,12 @@ class TrainEngine:
         if self.index_overlap:
             lo, _ = torch.cuda.Stream.priority_range()
             self._idx_stream = torch.cuda.Stream(self.device, priority=lo)
+            # the runtime sets a stream's hardware queue up at its first use: 0.2-5.6 ms of
+            # host time measured (tools/probes/bench_host_trace.py) -- here, not inside a run
+            self._idx_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._idx_stream):
+                torch.zeros(1, device=self.device).add_(1)
+            self._idx_stream.synchronize()
         self._ready = None           # (lo, hi, negatives version, side-stream event): _mark_built
         self._neg_version = 0
 
@@ -517,62 +523,38 @@ class TrainEngine:
         built it already, e.g. bench.py ahead of its timed region).  With index_overlap and
         prefetch (default: index), the index of the batches after each window -- the run's
         next window, or as many batches as the window after the run's last -- is built on the
-        side stream in slices, one in front of each graph replay (or graph_chunk eager steps),
-        so each slice runs beside the steps queued after it; one whole-window build beside
-        the steps slows them for its whole duration instead (measured: bench.py C3 17.4 ->
-        28 us/step).  With graph, every step runs inside a replayed HIP graph:
-        graph_chunk-step graphs and one graph per window remainder (last_advance: see
-        _cursor_replays)."""
+        side stream, queued in front of the window's steps so it runs beside them.  With
+        graph, every step runs inside a replayed HIP graph: graph_chunk-step graphs and one
+        graph per window remainder (last_advance: see _cursor_replays)."""
         self._ensure_epoch_mode()
         if self._dp:
             self._stale.update(("params", "acc"))
         pre = (index if prefetch is None else prefetch) and self.index_overlap
         replays = self._cursor_replays(first_batch, count, last_advance)
         wins = self.windows(first_batch, count)
-        st = self._stream()
         for wi, (b, n) in enumerate(wins):
             if index:
                 self._index_ready(b, n)
-            nxt = None
             if pre:
                 nn_ = wins[wi + 1][1] if wi + 1 < len(wins) else min(n, self.nb - (b + n))
-                nxt = (b + n, nn_) if nn_ > 0 else None
+                if nn_ > 0:
+                    self.prefetch_index(b + n, nn_)
             if graph and self.graph_chunk > 1 and self.graph_absolute:
-                chunks = [(lambda cb=cb, cn=cn: self._graph(cn, cb).replay())
-                          for cb, cn in self._chunks(b, n)]
-                for go, sl in zip(chunks, self._slices(nxt, len(chunks))):
-                    if sl:
-                        self.prefetch_index(*sl)
-                    go()
+                for cb, cn in self._chunks(b, n):
+                    self._graph(cn, cb).replay()
                 continue
             if self._cursor_at != b or self._moves_seen != self._moves():
                 self.set_cursor(b)
             self._cursor_at = None              # until the window's launches are queued
             if not graph or self.graph_chunk <= 1:
-                piece = self.graph_chunk if self.graph_chunk > 1 else 64
-                chunks = [(lambda c=min(piece, n - k): self._steps_eager(c, st))
-                          for k in range(0, n, piece)]
-                at = b + n
+                self._steps_eager(n, self._stream())
+                self._cursor_at = b + n
             else:
                 reps = replays[wi]
-                chunks = [(lambda c=cnt, a=adv: self._graph(c, advance=a).replay())
-                          for cnt, adv in reps]
-                at = b + n - (0 if reps[-1][1] else reps[-1][0])
-            for go, sl in zip(chunks, self._slices(nxt, len(chunks))):
-                if sl:
-                    self.prefetch_index(*sl)
-                go()
-            self._cursor_at = at
+                for cnt, adv in reps:
+                    self._graph(cnt, advance=adv).replay()
+                self._cursor_at = b + n - (0 if reps[-1][1] else reps[-1][0])
             self._moves_seen = self._moves()
-
-    @staticmethod
-    def _slices(nxt, k):
-        """[first, count) split into k consecutive slices (None where nothing is left)."""
-        if nxt is None:
-            return [None] * k
-        b, n = nxt
-        q = -(-n // k)
-        return [(b + i * q, min(q, n - i * q)) if i * q < n else None for i in range(k)]
 
     # ------------------------------------------------------------------ index overlap
     # self._ready = (lo, hi, negatives version, event): batches [lo, hi) have their row index

@@ -61,9 +61,3 @@ def test_prefetch_never_overwrites_the_window_in_flight(iw):
             written = {x % iw for x in range(b + n, b + n + n2)}
             assert not running & written
 
-
-def test_prefetch_slices_cover_the_next_window():
-    assert TrainEngine._slices(None, 3) == [None, None, None]
-    assert TrainEngine._slices((100, 512), 8) == [(100 + 64 * i, 64) for i in range(8)]
-    assert TrainEngine._slices((10, 5), 3) == [(10, 2), (12, 2), (14, 1)]
-    assert TrainEngine._slices((0, 2), 4) == [(0, 1), (1, 1), None, None]

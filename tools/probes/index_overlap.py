@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--dp-update", default="replicated")
     ap.add_argument("--n", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--graph-chunk", type=int, default=0, help="steps per graph (0: n)")
+    ap.add_argument("--slices", type=int, default=1, help="prefetch slices (one per graph)")
+    ap.add_argument("--priority", default="low", choices=["low", "normal"])
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     dev = torch.device("cuda", 0)
@@ -44,7 +47,8 @@ def main():
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
                              cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "ovl", cfg["dec"], False,
                              True, False, 1.0, device=dev, world_size=G, rank=0,
-                             exchange=NoPeers(G) if G > 1 else None, graph_chunk=args.n,
+                             exchange=NoPeers(G) if G > 1 else None,
+                             graph_chunk=args.graph_chunk or args.n,
                              mfma_bf16=cfg.get("bf16", False), dp_update=args.dp_update)
     ind.compile_function()
     eng = ind.engine
@@ -53,7 +57,7 @@ def main():
     assert 2 * n <= eng.index_window and 2 * n <= eng.nb, (eng.index_window, eng.nb)
     main_s = torch.cuda.current_stream(dev)
     lo, hi = torch.cuda.Stream.priority_range()
-    side = torch.cuda.Stream(dev, priority=lo)          # lowest priority
+    side = torch.cuda.Stream(dev, priority=lo if args.priority == "low" else 0)
     eng.build_index(0, 2 * n)
     eng.capture_for(0, n)
     eng.run(0, n, index=False)                          # warm
@@ -67,7 +71,18 @@ def main():
         _lib.check(eng.lib.rae_build_index(eng.plan, n, n, C.c_void_p(stream.cuda_stream)),
                    "rae_build_index")
 
-    res = {k: [] for k in ("steps", "index", "serial", "overlap")}
+    import time
+    res = {k: [] for k in ("steps", "index", "serial", "overlap", "overlap_sliced",
+                           "host_queue_sliced_us", "engine_sliced", "engine_sliced_host_us",
+                           "engine_sliced_own_stream", "engine_sliced_own_stream_host_us")}
+    own = torch.cuda.Stream(dev)
+    gc = args.graph_chunk or n
+
+    def build_slice(stream, b, c):
+        import ctypes as C
+        from rae import _lib
+        _lib.check(eng.lib.rae_build_index(eng.plan, b, c, C.c_void_p(stream.cuda_stream)),
+                   "rae_build_index")
     for _ in range(args.reps):
         torch.cuda.synchronize()
         a, b = ev(), ev()
@@ -102,6 +117,47 @@ def main():
         b.record(main_s)
         torch.cuda.synchronize()
         res["overlap"].append(a.elapsed_time(b) * 1e3 / n)
+
+        # sliced: one prefetch slice in front of each graph replay, as engine.run does
+        torch.cuda.synchronize()
+        a, b = ev(), ev()
+        a.record(main_s)
+        t0 = time.perf_counter()
+        eng.set_cursor(0)
+        k = max(1, args.slices)
+        q = -(-n // k)
+        cs = []
+        for g0 in range(0, n, gc):
+            i = g0 // gc
+            if i < k and i * q < n:
+                side.wait_stream(main_s)
+                build_slice(side, n + i * q, min(q, n - i * q))
+                c = ev()
+                c.record(side)
+                cs.append(c)
+            eng._graph(min(gc, n - g0)).replay()
+        res["host_queue_sliced_us"].append((time.perf_counter() - t0) * 1e6)
+        for c in cs:
+            main_s.wait_event(c)
+        b.record(main_s)
+        torch.cuda.synchronize()
+        eng.cursor_moved()
+        res["overlap_sliced"].append(a.elapsed_time(b) * 1e3 / n)
+
+        # the engine's own path: run(prefetch=True) on the default stream, then on a stream
+        for key, strm in (("engine_sliced", main_s), ("engine_sliced_own_stream", own)):
+            torch.cuda.synchronize()
+            with torch.cuda.stream(strm):
+                eng._ready = (0, n, eng._neg_version, None)
+                a, b = ev(), ev()
+                a.record(strm)
+                t0 = time.perf_counter()
+                eng.run(0, n, index=False, prefetch=True)
+                res[key + "_host_us"].append((time.perf_counter() - t0) * 1e6)
+                strm.wait_stream(eng._idx_stream)
+                b.record(strm)
+            torch.cuda.synchronize()
+            res[key].append(a.elapsed_time(b) * 1e3 / n)
     out = {k: float(np.median(v)) for k, v in res.items()}
     out.update(config=args.config, l=args.l, G=G, dp_update=args.dp_update, n=n,
                unit="us per step", kernel_forms=eng.kernel_forms_in_use())
