@@ -100,10 +100,15 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc_fast(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode_fast<D>(a, step_batch(a), blockIdx.x, smem);
 }
-template <bool BF16, bool DIRECT = false>
-__global__ __launch_bounds__(RAE_MTT) void k_bil_mt(StepArgs a, int pass) {
+#ifdef RAE_MT_WPE      // A/B: occupancy target of the M-tile passes (waves per SIMD)
+#define RAE_MT_ATTR __attribute__((amdgpu_waves_per_eu(RAE_MT_WPE)))
+#else
+#define RAE_MT_ATTR
+#endif
+template <bool BF16, bool DIRECT = false, bool DP = true>
+__global__ __launch_bounds__(RAE_MTT) RAE_MT_ATTR void k_bil_mt(StepArgs a, int pass) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bil_mt<BF16, DIRECT>(a, pass, smem);
+    bil_mt<BF16, DIRECT, DP>(a, pass, smem);
 }
 template <bool V4>
 __global__ __launch_bounds__(RAE_DBT) void k_bil_dec(StepArgs a) {
@@ -578,6 +583,7 @@ struct rae_plan {
     size_t smem_idx = 0;
     size_t smem_dec = 0;
     size_t smem_mt = 0;     // k_bil_mt: one 8 x 16 x m block of R in LDS
+    size_t smem_mt0 = 0;    // ... its first pass (no transposed image for dP): less LDS per WG
     bool mt_direct = false; // fp32 blocks beyond LDS (m > 320): k_bil_mt reads R from L2
     bool sp_split = false;  // SP forward as enc -> GEMM -> dec -> GEMM -> fin (large shapes)
     size_t smem_spe = 0;    // k_sp_enc
@@ -955,6 +961,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
     p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
     p->smem_mt = bil ? bil_mt_lds_bytes(c.relations, p->mt_bf16) : 0;
+    // the first pass never stages the transposed image (dP rides on the second): with half the
+    // LDS, two of its workgroups fit a CU and all (r/8)(r/16) start at once
+    p->smem_mt0 = (bil && p->mt_bf16) ? (size_t)RAE_MTI * RAE_MTJ * (((c.relations + 31) / 32 * 32) + 8) * 2
+                                      : p->smem_mt;
 
     if (p->smem_mt > RAE_MT_LDS_MAX) {        // fp32 block too large to stage (m > 320)
         p->mt_direct = true;
@@ -998,6 +1008,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
             (void)hipFuncSetAttribute((const void*)k_bil_dp2<8, 8>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)dp2_lds_bytes<8, 8>());
             (void)hipFuncSetAttribute((const void*)k_bil_mt<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
+            (void)hipFuncSetAttribute((const void*)k_bil_mt<true, false, false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
             (void)hipFuncSetAttribute((const void*)k_bil_mt<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_mt);
@@ -1105,7 +1117,9 @@ static void launch_fwd_bil(rae_plan* p, const StepArgs& a, hipStream_t st) {
     const dim3 gmt(((a.r + RAE_MTI - 1) / RAE_MTI) * ((a.r + RAE_MTJ - 1) / RAE_MTJ));
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) RAE_LAUNCH(p, (k_bil_dec<V4>), ge, dim3(RAE_DBT), p->smem_dec, st, a);
-        if (p->mt_bf16) RAE_LAUNCH(p, (k_bil_mt<true>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
+        if (p->mt_bf16 && pass == 0)       // no dP: the lighter instantiation, half the LDS
+            RAE_LAUNCH(p, (k_bil_mt<true, false, false>), gmt, dim3(RAE_MTT), p->smem_mt0, st, a, pass);
+        else if (p->mt_bf16) RAE_LAUNCH(p, (k_bil_mt<true>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
         else if (p->mt_direct) RAE_LAUNCH(p, (k_bil_mt<false, true>), gmt, dim3(RAE_MTT), 0, st, a, pass);
         else RAE_LAUNCH(p, (k_bil_mt<false>), gmt, dim3(RAE_MTT), p->smem_mt, st, a, pass);
     }

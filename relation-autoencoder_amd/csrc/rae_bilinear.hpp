@@ -238,7 +238,9 @@ __device__ __forceinline__ rae_bf16x8 to_bf16x8(float4 lo, float4 hi) {
 #define RAE_MTI 8         // rows i per block (a multiple of 4)
 #endif
 #define RAE_MTJ 16        // columns j per block (one MFMA tile of rows)
+#ifndef RAE_MTT
 #define RAE_MTT RAE_FBT   // threads per k_bil_mt workgroup (8 waves)
+#endif
 #define RAE_MTW (RAE_MTT / RAE_WAVE)
 #define RAE_MT_SB 8       // float4 staging loads per thread in flight per round
 // bf16: the block image [(i,j)][KP + 8] and, for the dP contraction of the second pass, its
@@ -267,7 +269,9 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
 #define RAE_MT_STAMP(slot) do { } while (0)
 #endif
 
-template <bool BF16, bool DIRECT = false>
+// DP: the instantiation that may carry the dP contraction (the second pass); the first pass's
+// instantiation has none of its registers (occupancy)
+template <bool BF16, bool DIRECT = false, bool DP = true>
 __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     static_assert(!(BF16 && DIRECT), "bf16 blocks are always staged (m <= 128)");
     const int r = a.r, m = a.m, l = a.l;
@@ -278,7 +282,7 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     const int it = blockIdx.x / nbj, jt = blockIdx.x - it * nbj;
     const int i0 = it * RAE_MTI, j0 = jt * RAE_MTJ;
     const int KP = (m + 31) / 32 * 32, ST = BF16 ? KP + 8 : m;   // row (i, j) stride in LDS
-    const bool tr = BF16 && pass == 1 && a.mtP != nullptr;        // stage the transpose too
+    const bool tr = DP && BF16 && pass == 1 && a.mtP != nullptr;  // stage the transpose too
     __bf16* sT = reinterpret_cast<__bf16*>(smem) + RAE_MTI * RAE_MTJ * ST;
     RAE_MT_STAMP(0);
     // ---- stage: LDS row (ii, jj) = R[i0+ii][j0+jj][0..m); rows past r are zero
@@ -347,7 +351,7 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
     // j0 + 8 (g&1) .. +7 and x / a1 at rows i0 + 2 ks + g/2, ks < RAE_MT_NKS (unconditional loads of
     // clamped addresses, then selects: a conditional load becomes a flat load through a zeroed
     // scratch slot)
-    const bool dpass = BF16 && pass == 1 && a.mtP != nullptr;
+    const bool dpass = DP && BF16 && pass == 1 && a.mtP != nullptr;
     struct DpOps { float a2v[8], yv[8], xq[RAE_MT_NKS], cq[RAE_MT_NKS]; };
     auto load_dp = [&](DpOps& o, const float* erb, bool bv) {
         const int jh = j0 + 8 * (g & 1);
@@ -474,7 +478,7 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                 *reinterpret_cast<float4*>(a.mtW + ((int64_t)it * l + bb) * a.r4 + j0 + 4 * g) = wacc;
         }
         RAE_MT_STAMP(5);
-        if constexpr (BF16) {
+        if constexpr (BF16 && DP) {
             if (dpass) {
                 // the block's share of dP_b[k] = sum_ij U_b[i][j] R[i][j][k], U = x a2^T + a1 y^T,
                 // from the same staged block (k_bil_dp2's contraction without another read of
