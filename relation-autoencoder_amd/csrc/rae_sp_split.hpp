@@ -138,7 +138,8 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
 // four summed in order -- so the split forward's own vectors and every rank's are bit-identical.
 // task = (example tile, embedding tile).
 #ifndef RAE_VR_KC
-#define RAE_VR_KC 8          // 16-deep K chunks whose operand loads one round issues
+#define RAE_VR_KC 4          // 16-deep K chunks whose operand loads one round issues (4: 128
+                             // registers, 4 waves per SIMD; 8: 168, 3)
 #endif
 static_assert(RAE_VR_KC % 4 == 0, "chunk u of a round feeds accumulator u % 4");
 __host__ __device__ inline int vrec_tasks(int L, int r) { return ((L + 15) / 16) * ((r + 15) / 16); }
@@ -154,26 +155,40 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     const float* C1r = a.C1 + (int64_t)(iv ? i : 0) * m;
     const float* C2r = a.C2 + (int64_t)(iv ? i : 0) * m;
     const int nch = (m + 15) / 16;
+    // the coefficients of the tile's four output rows first: independent of the products
+    float dlv[4], drv[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int bo = bt * 16 + 4 * g + reg;
+        const float* rec = a.ex + (int64_t)(bo < L ? bo : 0) * a.lay.rec + a.lay.oAux;
+        dlv[reg] = rec[0];
+        drv[reg] = rec[1];
+    }
     rae_f32x4 acc1[4], acc2[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc1[q] = acc2[q] = rae_f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c0 = 0; c0 < nch; c0 += RAE_VR_KC) {          // one round at m <= 128
-        float4 x[RAE_VR_KC], y1[RAE_VR_KC], y2[RAE_VR_KC];
+    for (int c0 = 0; c0 < nch; c0 += RAE_VR_KC) {          // one round at m <= 16 RAE_VR_KC
+        // V1's operands (P and C1) in one round trip, then C2's into the same registers: the
+        // P fragments serve both products (fewer live registers: more resident waves)
+        float4 x[RAE_VR_KC], y[RAE_VR_KC];
 #pragma unroll
         for (int u = 0; u < RAE_VR_KC; ++u) {
             const int k = (c0 + u) * 16 + 4 * g;           // >= m past the last chunk
             const bool cv = c0 + u < nch;
             x[u] = load4_guard<VEC>(Pr, k, m, bv && cv);
-            y1[u] = load4_guard<VEC>(C1r, k, m, iv && cv);
-            y2[u] = load4_guard<VEC>(C2r, k, m, iv && cv);
+            y[u] = load4_guard<VEC>(C1r, k, m, iv && cv);
         }
 #pragma unroll
-        for (int u = 0; u < RAE_VR_KC; ++u) {             // RAE_VR_KC % 4 == 0: chunk c0 + u
-            if (c0 + u < nch) {                            // -> accumulator u % 4
-                acc1[u & 3] = mfma4_f32(x[u], y1[u], acc1[u & 3]);
-                acc2[u & 3] = mfma4_f32(x[u], y2[u], acc2[u & 3]);
-            }
+        for (int u = 0; u < RAE_VR_KC; ++u)                // RAE_VR_KC % 4 == 0: chunk c0 + u
+            if (c0 + u < nch) acc1[u & 3] = mfma4_f32(x[u], y[u], acc1[u & 3]);   // -> acc u % 4
+#pragma unroll
+        for (int u = 0; u < RAE_VR_KC; ++u) {
+            const int k = (c0 + u) * 16 + 4 * g;
+            y[u] = load4_guard<VEC>(C2r, k, m, iv && c0 + u < nch);
         }
+#pragma unroll
+        for (int u = 0; u < RAE_VR_KC; ++u)
+            if (c0 + u < nch) acc2[u & 3] = mfma4_f32(x[u], y[u], acc2[u & 3]);
     }
     // sp_gemm_combine's order: wave 0's accumulator, + wave 1's, + wave 2's, + wave 3's
     rae_f32x4 o1 = acc1[0], o2 = acc2[0];
@@ -187,12 +202,10 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][i = li]
         const int bo = bt * 16 + 4 * g + reg;
         if (bo < L && iv) {
-            const float* rec = a.ex + (int64_t)bo * a.lay.rec;
-            const float dl = rec[a.lay.oAux + 0], dr = rec[a.lay.oAux + 1];
             float* v = vb + (int64_t)bo * a.vbs;
             v[a.vV1 + i] = o1[reg];
             v[a.vV2 + i] = o2[reg];
-            v[a.vG1 + i] = dl * o1[reg] + dr * o2[reg];
+            v[a.vG1 + i] = dlv[reg] * o1[reg] + drv[reg] * o2[reg];
         }
     }
 }
