@@ -105,16 +105,17 @@ typedef struct rae_config {
                                 * replicas after every step)                                  */
 #define RAE_DPUPD_PARTITIONED 1 /* rank k updates the rows it owns (row % G == k) and pushes *
                                  * the next step's rows to the ranks that read them            */
-#define RAE_PRIV_AUTO 0       /* every plan without a regulariser (lambda1 = lambda2 = 0) and   *
-                               * with 2 + 2s <= 64 record slots, any decoder: a row exactly one *
-                               * record of the global batch references is left out of the      *
-                               * update's row tasks and updated by per-example workgroups of the*
-                               * same update launch (task_private_rows; same arithmetic as the  *
-                               * one-record row task, bit-identical parameters).  Several ranks:*
-                               * every rank's update takes the private rows it updates (the     *
-                               * replicated update all of them, the partitioned one its own,   *
-                               * one workgroup per example)                                     */
-#define RAE_PRIV_OFF 1        /* every row updated by the update launch                        */
+#define RAE_PRIV_AUTO 0       /* rows exactly one record of the global batch references are left  *
+                               * out of the update's row tasks and updated by per-example        *
+                               * workgroups of the same update launch (task_private_rows; the    *
+                               * one-record row task's arithmetic, bit-identical parameters) in  *
+                               * single-rank and replicated plans with a global batch below 4096 *
+                               * examples, without a regulariser (lambda1 = lambda2 = 0) and     *
+                               * with 2 + 2s <= 64 record slots, any decoder                     */
+#define RAE_PRIV_OFF 1        /* every row updated by the update's row tasks                      */
+#define RAE_PRIV_ON 2         /* private rows whenever admissible (no regulariser, <= 64 slots),   *
+                               * any global batch; the partitioned update takes the private rows *
+                               * it owns, one wave per example                                    */
 #define RAE_DPDENSE_AUTO 0    /* partials when they are at most half of dw1 / dw2 in the records *
                                * (per-rank partial chunk <= r floats: l >~ 2 relations)          */
 #define RAE_DPDENSE_RECORDS 1 /* dw1 / dw2 of every example in the exchange records; the update *

@@ -225,6 +225,9 @@ __host__ __device__ inline int update_wave_free_tasks(int dec, int r, int m) {
 #ifndef RAE_HCH
 #define RAE_HCH 128           // very heavy rows above this many records are split into chunks
 #endif
+#ifndef RAE_PRIV_MAXL
+#define RAE_PRIV_MAXL 4096    // private rows (auto) below this global batch (equal at 4096)
+#endif
 #ifndef RAE_HCH_MINL
 #define RAE_HCH_MINL 2048     // ... in plans with a global batch of at least this many examples
 #endif
@@ -665,7 +668,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.bil_dp < RAE_BILDP_AUTO || c.bil_dp > RAE_BILDP_MTILE ||
         c.bil_prep < RAE_BILPREP_AUTO || c.bil_prep > RAE_BILPREP_KERNEL ||
         c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED ||
-        c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_OFF ||
+        c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_ON ||
         c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS ||
         c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
@@ -853,7 +856,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // the example's features from its descriptor (<= dcap, <= 32).  Several ranks: every rank's
     // update takes the private rows it updates (replicated: all; partitioned: its own), so the
     // descriptors cover the whole global batch
-    a.priv = (!a.reg_on && NJ <= 64 && c.priv_rows == RAE_PRIV_AUTO) ? 1 : 0;
+    // auto: single-rank and replicated plans below a global batch of RAE_PRIV_MAXL; at larger
+    // batches and in the partitioned update (a rank's own private rows: a few per example) the
+    // row tasks do them faster (profiles/r04_ab.txt)
+    const bool priv_ok = !a.reg_on && NJ <= 64;
+    a.priv = (priv_ok && (c.priv_rows == RAE_PRIV_ON ||
+                          (c.priv_rows == RAE_PRIV_AUTO && !a.part && L < RAE_PRIV_MAXL))) ? 1 : 0;
     a.dnx = (a.priv && c.world_size > 1) ? L : c.batch_size;
     a.d0 = a.dnx == L ? c.rank * c.batch_size : 0;
     const size_t o_desc = take(4ull * W_ * a.dnx * a.dstride);
@@ -1037,7 +1045,7 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
     out->bil_prep = (!bil || !p->args.bf16) ? 0 : (p->args.fuse_prep ? RAE_BILPREP_AUTO
                                                                     : RAE_BILPREP_KERNEL);
     out->dp_update = p->cfg.dp_update;
-    out->priv_rows = p->args.priv ? RAE_PRIV_AUTO : RAE_PRIV_OFF;
+    out->priv_rows = p->args.priv ? RAE_PRIV_ON : RAE_PRIV_OFF;
     out->dp_dense = p->args.lay.wire == 2 ? RAE_DPDENSE_PARTIALS
                   : (p->args.lay.wire == 1 ? RAE_DPDENSE_RECORDS : 0);
     out->heavy_chunk = p->args.hch ? RAE_HCHUNK_ON : RAE_HCHUNK_OFF;

@@ -101,7 +101,7 @@ KERNEL_FORMS = {
     "bil_dp": {"auto": 0, "strided": 1, "staged": 2, "mtile": 3},
     "bil_prep": {"auto": 0, "kernel": 1},
     "dp_update": {"replicated": 0, "partitioned": 1},
-    "priv_rows": {"auto": 0, "off": 1},
+    "priv_rows": {"auto": 0, "off": 1, "on": 2},
     "dp_dense": {"auto": 0, "records": 1, "partials": 2},
     "heavy_chunk": {"auto": 0, "off": 1, "on": 2},
 }

@@ -276,7 +276,7 @@ class TrainEngine:
         TrainEngine(kernel_forms=...) / bench.py --kernel-form to pin the same run:
         sp_forward fused|split (SP), bil_dp strided|staged|mtile (bilinear), bil_prep
         auto|kernel (bf16 bilinear: the forward writes the R-gradient operands, or k_bil_prep
-        does), dp_update replicated|partitioned, priv_rows auto|off (rows one record of the
+        does), dp_update replicated|partitioned, priv_rows on|off (rows one record of the
         batch references updated per example, or by the row tasks), dp_dense records|partials
         (data-parallel SP: dw1 / dw2 per example in the exchange, or each rank's reduced dense
         gradients), heavy_chunk off|on (rows with more than 128 records of the global batch

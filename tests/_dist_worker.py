@@ -183,7 +183,7 @@ def run_sync_rows(out):
     np.savez(os.path.join(out, f"rows_{rk}.npz"), recv=recv.numpy(), t2=t2.numpy(), t1=t1.numpy())
 
 
-def run_gpu(out, decoder, dp_update="replicated", dense="auto"):
+def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto"):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -196,10 +196,13 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto"):
                              m, s, 0.0, 0.0, "adagrad", "dp", decoder, False, True, False, 1.0,
                              device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
                              dp_update=dp_update,
-                             kernel_forms={"dp_dense": dense} if decoder == "sp" else None)
+                             kernel_forms=dict({"dp_dense": dense} if decoder == "sp" else {},
+                                               priv_rows=priv))
     ind.learn(verbose=False)
     if decoder == "sp" and dense != "auto":
         assert ind.engine.kernel_forms_in_use()["dp_dense"] == dense
+    if priv != "auto":
+        assert ind.engine.kernel_forms_in_use()["priv_rows"] == priv
     ind.engine.sync_replicas()
     params = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
     np.savez(os.path.join(out, f"gpu_{dp_update}_{decoder}_{rk}.npz"),
@@ -354,7 +357,8 @@ def main():
             run_sync_rows(out)
         elif mode == "gpu":
             run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated",
-                    sys.argv[5] if len(sys.argv) > 5 else "auto")
+                    sys.argv[5] if len(sys.argv) > 5 else "auto",
+                    sys.argv[6] if len(sys.argv) > 6 else "auto")
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
                        heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")

@@ -619,7 +619,7 @@ def test_private_rows_match_update_launch(built_lib, cuda_dev, opt, values, dec,
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     out = []
-    for form in ("auto", "off"):
+    for form in ("on", "off"):
         data, gold = synthetic_dataset(400, 3000, 10, seed=21)
         if values:                                   # non-binary features: x_f != 1
             x = data.split["train"].xFeats
