@@ -261,7 +261,9 @@ def main():
     ws, rk, lrank = rdist.init()
     if ws != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
-    dev = torch.device("cuda", lrank)
+    # one GPU per local rank; ranks beyond the node's GPUs share them (a rehearsal of the
+    # multi-rank path on a one-GPU box, RAE_DIST_BACKEND=gloo)
+    dev = torch.device("cuda", lrank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
     l = args.batch_size

@@ -36,6 +36,8 @@ def init(backend: str | None = None):
     ws, rk, lr = env_world()
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # RAE_DIST_BACKEND=gloo: host-staged collectives (ranks sharing one GPU, tests only)
+        backend = backend or os.environ.get("RAE_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {}
