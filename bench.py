@@ -97,19 +97,28 @@ def step_flops(L, l, m, r, dec):
     return 2 * r * r * m * (2 * l + L)
 
 
-def pmc_traffic(config):
+def pmc_traffic(config, batch_size=100):
     """L2-to-fabric (HBM + Infinity Cache) bytes per launch from the newest committed
-    rocprofv3 PMC passes (profiles/rNN_<config>_pmc_traffic.json), if any:
+    rocprofv3 PMC passes (profiles/rNN_<config>_pmc_traffic.json) taken at this per-rank batch
+    size (the passes' bench arguments name it; none means the default 100), if any:
     2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half of a wide
     coalesced read on gfx950; the same pass's rae_stream_copy, of known bytes, confirms the
     factor), averaged over the launches of each kernel."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc_traffic.json")))
-    if not paths:
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc_traffic.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_l*_pmc_traffic.json")))
+    found = None
+    for path in paths:
+        with open(path) as fh:
+            out = json.load(fh)
+        src = out.get("source", "")
+        bs = int(src.split("--batch-size", 1)[1].split()[0]) if "--batch-size" in src else 100
+        if bs == batch_size and (found is None or os.path.basename(path)[:3] >= found[0]):
+            found = (os.path.basename(path)[:3], path, out)
+    if found is None:
         return None
-    with open(paths[-1]) as fh:
-        out = json.load(fh)
-    out["file"] = os.path.relpath(paths[-1], ROOT)
+    _, path, out = found
+    out["file"] = os.path.relpath(path, ROOT)
     return out
 
 
@@ -399,7 +408,7 @@ def main():
            for i in range(n_it)]
     by = np.array([p_["s8d"] for p_ in per], dtype=np.float64).mean(axis=0)
     bmin = np.array([p_["min"] for p_ in per], dtype=np.float64).mean(axis=0)
-    traffic = pmc_traffic(args.config)
+    traffic = pmc_traffic(args.config, args.batch_size)
     build_id = lib.rae_build_id().decode()
     kern = {}
     for i, (name, us) in enumerate((("k_forward", fwd_us), ("k_update", upd_us))):

@@ -27,7 +27,7 @@ for st in "$@"; do
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $p -f csv -d $O/pmc_$c/$p -o run \
           -- python3 $R/bench.py $BA > $O/pmc_${c}_$p.log 2>&1) || { echo "pmc $c $p failed"; tail -20 $O/pmc_${c}_$p.log; exit 1; }
       done
-      python3 tools/pmc_traffic.py $O/pmc_$c/FETCH_SIZE $O/pmc_$c/WRITE_SIZE --config $c \
+      python3 tools/pmc_traffic.py $O/pmc_$c/FETCH_SIZE $O/pmc_$c/WRITE_SIZE $BA \
         --out $O/r04_${c}_pmc_traffic.json > $O/pmc_${c}_post.log 2>&1 || { echo "pmc $c post failed"; tail -20 $O/pmc_${c}_post.log; exit 1; }
       cp $O/r04_${c}_pmc_traffic.json profiles/
       python3 -c "
