@@ -183,7 +183,7 @@ def run_sync_rows(out):
     np.savez(os.path.join(out, f"rows_{rk}.npz"), recv=recv.numpy(), t2=t2.numpy(), t1=t1.numpy())
 
 
-def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto"):
+def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", index_window=0):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -197,7 +197,8 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto"):
                              device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
                              dp_update=dp_update,
                              kernel_forms=dict({"dp_dense": dense} if decoder == "sp" else {},
-                                               priv_rows=priv))
+                                               priv_rows=priv),
+                             index_window=index_window)
     ind.learn(verbose=False)
     if decoder == "sp" and dense != "auto":
         assert ind.engine.kernel_forms_in_use()["dp_dense"] == dense
@@ -358,7 +359,8 @@ def main():
         elif mode == "gpu":
             run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated",
                     sys.argv[5] if len(sys.argv) > 5 else "auto",
-                    sys.argv[6] if len(sys.argv) > 6 else "auto")
+                    sys.argv[6] if len(sys.argv) > 6 else "auto",
+                    int(sys.argv[7]) if len(sys.argv) > 7 else 0)
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
                        heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")

@@ -126,23 +126,26 @@ def test_gpu_ranks_match_global_batch(built_lib, cuda_dev, tmp_path, decoder, ws
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder,ws,dense,priv", [("sp", 2, "auto", "auto"),
-                                                   ("rescal+sp", 2, "auto", "auto"),
-                                                   ("sp", 4, "auto", "auto"),
-                                                   ("rescal", 4, "auto", "auto"),
-                                                   ("sp", 8, "auto", "auto"),
-                                                   ("sp", 4, "partials", "auto"),
-                                                   ("sp", 8, "partials", "auto"),
-                                                   ("sp", 4, "auto", "on"),
-                                                   ("rescal", 2, "auto", "on")])
-def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dense, priv):
+@pytest.mark.parametrize("decoder,ws,dense,priv,iw", [("sp", 2, "auto", "auto", 0),
+                                                      ("rescal+sp", 2, "auto", "auto", 0),
+                                                      ("sp", 4, "auto", "auto", 0),
+                                                      ("rescal", 4, "auto", "auto", 0),
+                                                      ("sp", 8, "auto", "auto", 0),
+                                                      ("sp", 4, "partials", "auto", 0),
+                                                      ("sp", 8, "partials", "auto", 0),
+                                                      ("sp", 4, "auto", "on", 0),
+                                                      ("rescal", 2, "auto", "on", 0),
+                                                      ("sp", 2, "auto", "auto", 4)])
+def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dense, priv, iw):
     """The HIP path with the row-owner partitioned update (k_build_dplists, k_dp_move, the
     owned-rows row index) on `ws` ranks sharing the GPU: == the oracle at the global batch,
     and bit-identical to the replicated update's parameters and costs (priv "on": the
     partitioned update's own private rows per example, compact form, against the replicated
-    update's)."""
-    _launch(["gpu", str(tmp_path), decoder, "partitioned", dense, priv], nproc=ws)
-    _launch(["gpu", str(tmp_path), decoder, "replicated", dense, priv], nproc=ws)
+    update's; iw = 4: a ring of four batches, so every epoch runs many windows with the next
+    window's index and row lists built beside the steps and the row-list capacities agreed per
+    window)."""
+    _launch(["gpu", str(tmp_path), decoder, "partitioned", dense, priv, str(iw)], nproc=ws)
+    _launch(["gpu", str(tmp_path), decoder, "replicated", dense, priv, str(iw)], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
     gp = [np.load(tmp_path / f"gpu_partitioned_{decoder}_{k}.npz") for k in range(ws)]
     gr = np.load(tmp_path / f"gpu_replicated_{decoder}_0.npz")
