@@ -86,7 +86,7 @@ class ReconstructInducer:
         self.mfma_bf16 = bool(mfma_bf16)   # RESCAL / hybrid: bf16 MFMA operands (config 5)
         self.kernel_forms = dict(kernel_forms or {})   # engine.TrainEngine kernel_forms
         self.index_window = int(index_window)          # engine.TrainEngine row-index ring
-        self.index_overlap = bool(index_overlap)
+        self.index_overlap = bool(index_overlap)       # next window's index beside the steps
         self.dp_update = dp_update         # "replicated" | "partitioned" (rae/dist.py)
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
