@@ -263,6 +263,44 @@ def test_c3_global_batch_800(built_lib, cuda_dev, heavy_chunk):
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
 
 
+@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
+def test_bilinear_heavy_chunks(built_lib, cuda_dev, dec):
+    """The bilinear updates with the heavy-row chunks (heavy_chunk on: rows with > 128 records of
+    the global batch summed as parallel chunks, k_heavy_fin combining them) against the same
+    run without them, at a Zipf global batch of 800 from the 1M-triple generator: costs and
+    every parameter equal to fp32 summation-order noise (a lost or doubled chunk would not be)."""
+    import torch
+    from rae.data import synthetic_dataset
+    from rae.inducer import ReconstructInducer
+    runs = {}
+    for hc in ("off", "on"):
+        data, gold = synthetic_dataset(1_000_000, 2 ** 17, 100, seed=1234)
+        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 800, 64, 30, 20,
+                                 0.0, 0.0, "adagrad", "hchunk", dec, False, True, False, 1.0,
+                                 device=cuda_dev, graph_chunk=2, kernel_forms={"heavy_chunk": hc})
+        ind.compile_function()
+        eng = ind.engine
+        assert eng.kernel_forms_in_use()["heavy_chunk"] == hc
+        n1, n2 = ind.draw_epoch_negatives()
+        if hc == "off":   # the batches do have rows past one chunk (the path is exercised)
+            xs = data.split["train"]
+            ids = np.concatenate([xs.args1[:800], xs.args2[:800], np.ravel(n1[:, :800]),
+                                  np.ravel(n2[:, :800])])
+            assert np.bincount(ids).max() > 128
+        eng.set_epoch_negatives(n1, n2)
+        eng.run(0, 3)
+        torch.cuda.synchronize()
+        eng.check()
+        runs[hc] = ({k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()},
+                    eng.costs[:3].cpu().numpy().astype(np.float64))
+        ind._drop_engine()
+    (p0, c0), (p1, c1) = runs["off"], runs["on"]
+    np.testing.assert_allclose(c1, c0, rtol=1e-5, atol=1e-6)
+    for k in p0:
+        err = np.abs(p1[k] - p0[k])
+        assert np.all(err <= 1e-5 + 1e-4 * np.abs(p0[k])), f"{k}: max err {err.max():.3e}"
+
+
 # --------------------------------------------------------------------------------------------
 # config C4 at its real size: 10M synthetic triples, d = 2^20, K = 300, embed 300, neg 50, l=100
 # --------------------------------------------------------------------------------------------
