@@ -263,8 +263,9 @@ def test_c3_global_batch_800(built_lib, cuda_dev, heavy_chunk):
     _check(want_c, got_c, want_p, got_p, init, min_untouched=0.5)
 
 
-@pytest.mark.parametrize("dec", ["rescal", "rescal+sp"])
-def test_bilinear_heavy_chunks(built_lib, cuda_dev, dec):
+@pytest.mark.parametrize("dec,opt", [("rescal", "adagrad"), ("rescal+sp", "adagrad"),
+                                     ("sp", "sgd"), ("rescal", "sgd")])
+def test_bilinear_heavy_chunks(built_lib, cuda_dev, dec, opt):
     """The bilinear updates with the heavy-row chunks (heavy_chunk on: rows with > 128 records of
     the global batch summed as parallel chunks, k_heavy_fin combining them) against the same
     run without them, at a Zipf global batch of 800 from the 1M-triple generator: costs and
@@ -276,7 +277,7 @@ def test_bilinear_heavy_chunks(built_lib, cuda_dev, dec):
     for hc in ("off", "on"):
         data, gold = synthetic_dataset(1_000_000, 2 ** 17, 100, seed=1234)
         ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, 800, 64, 30, 20,
-                                 0.0, 0.0, "adagrad", "hchunk", dec, False, True, False, 1.0,
+                                 0.0, 0.0, opt, "hchunk", dec, False, True, False, 1.0,
                                  device=cuda_dev, graph_chunk=2, kernel_forms={"heavy_chunk": hc})
         ind.compile_function()
         eng = ind.engine
