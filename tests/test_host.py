@@ -100,3 +100,16 @@ def test_checkpoint_round_trip_cpu(tmp_path):
         assert torch.equal(x, y)
     assert b.cur_epoch == 1 and b.train_errors == [3.5]
     assert np.array_equal(a.rng.uniform(size=5), b.rng.uniform(size=5))
+
+
+def test_bench_attaches_traffic_of_the_same_batch_size():
+    """bench.py's roofline 'traffic' comes from the committed PMC passes taken at the run's own
+    per-rank batch size (the passes' bench arguments name it; none = the default 100)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    t = bench.pmc_traffic("c3", 100)
+    assert t is not None and "--batch-size" not in t["source"]
+    t8 = bench.pmc_traffic("c3", 800)
+    assert t8 is not None and "--batch-size 800" in t8["source"]
+    assert bench.pmc_traffic("c3", 37) is None
