@@ -123,9 +123,10 @@ typedef struct rae_config {
 #define RAE_DPDENSE_PARTIALS 2 /* each rank reduces its own l examples' dC1 / dC2 / dWb before   *
                                 * the exchange (k_dpart); the records carry the partial block,  *
                                 * the update sums the ranks' blocks in rank order               */
-#define RAE_HCHUNK_AUTO 0     /* global batches of >= 2048 examples: rows with more than 128     *
-                               * records of the batch summed as 128-record chunks in parallel    *
-                               * (one partial per chunk, k_heavy_fin adds them in chunk order and *
+#define RAE_HCHUNK_AUTO 0     /* global batches of >= 2048 examples: rows with at least 256      *
+                               * records of the batch summed as floor(records / 128) chunks in   *
+                               * parallel (128 records each, the last one to the row's end; one  *
+                               * partial per chunk, k_heavy_fin adds them in chunk order and     *
                                * applies the optimiser); smaller batches: off                    */
 #define RAE_HCHUNK_OFF 1      /* every very heavy row summed by one workgroup                      */
 #define RAE_HCHUNK_ON 2       /* chunks at any global batch                                        */
@@ -249,8 +250,11 @@ int rae_event_create(void** event_out);
 int rae_event_destroy(void* event);
 /* waits for stop_event, then *ms = hipEventElapsedTime(start_event, stop_event) */
 int rae_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
-/* Device error word (overflow flags); host reads it with rae_check(). */
+/* Device error word (overflow flags); host reads it with rae_check() (a blocking read: waits
+ * for all the device's queued work) or rae_check_on() (ordered on `stream` only: waits for
+ * the work queued on that stream, e.g. a row-index build on a side stream).              */
 int rae_check(rae_plan* plan);
+int rae_check_on(rae_plan* plan, rae_stream_t stream);
 
 /* --- negative sampling (learning/NegativeExampleGenerator.py:14-32) ----------------- */
 /* out[i] = first j with cum[j] >= x_i  (numpy searchsorted side='left' over the float64 CDF

@@ -581,6 +581,7 @@ struct rae_plan {
     int64_t cursor_moves = 0;  // host count of rae_set_cursor / rae_advance_cursor calls
     int64_t* d_zero = nullptr;
     int* d_err = nullptr;
+    int* h_err = nullptr;   // pinned host word of rae_check_on
     char* ws = nullptr;
     size_t smem_fwd = 0;
     size_t smem_idx = 0;
@@ -829,8 +830,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         const int Lo = a.part ? (L + a.G - 1) / a.G : L;     // the rows this rank updates
         const int nvc = Lo / RAE_NVC_DIV > RAE_NVC_MIN ? Lo / RAE_NVC_DIV : RAE_NVC_MIN;
         a.NVC = nvc < a.VCA + a.VCW ? nvc : a.VCA + a.VCW;
-        // large global batches: very heavy rows with more than RAE_HCH records split into
-        // chunks (every chunk a workgroup task: they need NVC >= all chunks of a batch)
+        // large global batches: very heavy rows with at least 2 RAE_HCH records split into
+        // floor(records / RAE_HCH) chunks (every chunk a workgroup task: NVC >= HF + 1 >
+        // records / RAE_HCH, the most chunks a batch can have -- rae_index.hpp build_batch_tasks)
         a.hch = (c.heavy_chunk == RAE_HCHUNK_ON ||
                  (c.heavy_chunk == RAE_HCHUNK_AUTO && L >= RAE_HCH_MINL)) ? RAE_HCH : 0;
         if (a.hch) {
@@ -918,6 +920,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_HIP, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
     }
     (void)hipMemset(p->ws, 0, off);
+    e = hipHostMalloc(reinterpret_cast<void**>(&p->h_err), sizeof(int), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipFree(p->ws);
+        delete p;
+        return fail(RAE_E_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    *p->h_err = 0;
     p->d_cursor = reinterpret_cast<int64_t*>(p->ws + o_cursor);
     p->d_zero = reinterpret_cast<int64_t*>(p->ws + o_zero);
     p->d_err = reinterpret_cast<int*>(p->ws + o_err);
@@ -1055,6 +1064,7 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
 extern "C" int rae_plan_destroy(rae_plan* p) {
     if (!p) return RAE_OK;
     if (p->ws) (void)hipFree(p->ws);
+    if (p->h_err) (void)hipHostFree(p->h_err);
     delete p;
     return RAE_OK;
 }
@@ -1439,15 +1449,27 @@ extern "C" int rae_debug_grid(rae_plan* p, int* out) {
 }
 #endif
 
-extern "C" int rae_check(rae_plan* p) {
-    if (!p) return fail(RAE_E_INVALID, "null plan");
-    int e = 0;
-    HIPCHK(hipMemcpy(&e, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
+static int err_flags(int e) {
     if (e) return fail(RAE_E_OVERFLOW, std::string(e & 8 ? "a data-parallel row list overflowed "
                                                          "its capacity; " : "") +
                                            "row-index partition overflow (flags=" +
                                            std::to_string(e) + ")");
     return RAE_OK;
+}
+extern "C" int rae_check(rae_plan* p) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    int e = 0;
+    HIPCHK(hipMemcpy(&e, p->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    return err_flags(e);
+}
+// the same read ordered on one stream (pinned host word): the caller waits for that stream's
+// queued work only
+extern "C" int rae_check_on(rae_plan* p, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    HIPCHK(hipMemcpyAsync(p->h_err, p->d_err, sizeof(int), hipMemcpyDeviceToHost,
+                          (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return err_flags(*p->h_err);
 }
 
 static int launch_neg(const double* cum, int64_t n, const double* u, uint64_t seed,

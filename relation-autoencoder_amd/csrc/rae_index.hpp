@@ -355,9 +355,14 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
         if (v >= VA) sg.x = ~sg.x;
         return sg;
     };
-    // very heavy rows: rows with more than hch records become chunk tasks (the first vtask
-    // entries) plus a combine entry; the others keep one workgroup task each, overflowing to
-    // wave tasks beyond NVC
+    // very heavy rows: rows with at least 2 hch records become floor(records / hch) chunk tasks
+    // (the first vtask entries; chunk k = records [st + k hch, st + (k+1) hch), the last one
+    // to the row's end: hch .. 2 hch - 1 records) plus a combine entry; the others keep one
+    // workgroup task each, overflowing to wave tasks beyond NVC.  With floor counting a batch
+    // has at most records / hch < HF < NVC chunks and fewer than HF chunked rows (rae.hip sizes
+    // NVC >= HF + 1), so every chunk and combine entry has its slot (ceil counting
+    // could exceed NVC and leave k_heavy_fin reading partials no chunk task wrote).
+    auto nchunks = [&](int cnt) { return (a.hch > 0 && cnt >= 2 * a.hch) ? cnt / a.hch : 0; };
     int NC = 0, NF = 0, NU = 0;
     if (a.hch > 0) {
         int4* hf = reinterpret_cast<int4*>(a.hfin) + slot * a.HF;
@@ -367,24 +372,20 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
             int nch = 0;
             if (v < VA + VW) {
                 sg = vrow(v);
-                const int cnt = sg.z - sg.y;
-                nch = cnt > a.hch ? (cnt + a.hch - 1) / a.hch : 0;
+                nch = nchunks(sg.z - sg.y);
             }
             int tc, tf;
             const int cb = NC + block_int_scan<BT>(nch, sws, &tc);
             const int fb = NF + block_int_scan<BT>(nch > 0 ? 1 : 0, sws, &tf);
             for (int k = 0; k < nch; ++k) {
                 const int c = cb + k;
-                if (c < a.NVC)
-                    vt[c] = make_int4(sg.x, sg.y + k * a.hch, min(sg.y + (k + 1) * a.hch, sg.z), -1 - c);
+                const int e = (k + 1 == nch) ? sg.z : sg.y + (k + 1) * a.hch;
+                vt[c] = make_int4(sg.x, sg.y + k * a.hch, e, -1 - c);
             }
-            if (nch > 0 && fb < a.HF) hf[fb] = make_int4(sg.x, cb, nch, 0);
+            if (nch > 0) hf[fb] = make_int4(sg.x, cb, nch, 0);
             NC += tc;
             NF += tf;
         }
-        if (threadIdx.x == 0 && (NC > a.NVC || NF > a.HF)) atomicOr(a.err, 32);
-        NC = min(NC, a.NVC);
-        NF = min(NF, a.HF);
     }
     for (int v0 = 0; v0 < VA + VW; v0 += BT) {        // the unchunked very heavy rows
         const int v = v0 + threadIdx.x;
@@ -392,7 +393,7 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
         bool un = false;
         if (v < VA + VW) {
             sg = vrow(v);
-            un = a.hch <= 0 || sg.z - sg.y <= a.hch;
+            un = nchunks(sg.z - sg.y) == 0;
         }
         int tu;
         const int i = NC + NU + block_int_scan<BT>(un ? 1 : 0, sws, &tu);

@@ -185,6 +185,9 @@ __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, const D& Dm, 
 #ifndef RAE_KO_A
 #define RAE_KO_A 0
 #endif
+#if (RAE_KO_C || RAE_KO_W || RAE_KO_A) && !defined(RAE_DIAG)
+#error "RAE_KO_C / RAE_KO_W / RAE_KO_A are timing knockouts with wrong results: a diagnostic build (-DRAE_DIAG)"
+#endif
 
 // ---- decoder weight matrices C1, C2 (r, m) in registers ----------------------------------
 // group gid (16 lanes) owns rows i = gid + NG*ra, lane q owns column vectors c = q + 16*cc.

@@ -70,7 +70,7 @@ EXPORTS = (
     "rae_exchange_record_floats", "rae_exchange_floats", "rae_set_negatives",
     "rae_set_cursor", "rae_advance_cursor", "rae_cursor_moves", "rae_step_forward",
     "rae_step_update", "rae_step_forward_at", "rae_step_update_at",
-    "rae_train_step", "rae_check", "rae_label", "rae_build_index", "rae_index_window",
+    "rae_train_step", "rae_check", "rae_check_on", "rae_label", "rae_build_index", "rae_index_window",
     "rae_neg_sample", "rae_neg_sample_philox",
     "rae_time_next", "rae_event_create", "rae_event_destroy", "rae_event_elapsed_ms",
     "rae_stream_copy", "rae_mfma_probe", "rae_plan_forms",
@@ -173,6 +173,7 @@ def load(path: str | None = None):
     lib.rae_step_update_at.argtypes = [_P, C.c_int64, _P]
     lib.rae_train_step.argtypes = [_P, C.c_int64, _P, _P, _P]
     lib.rae_check.argtypes = [_P]
+    lib.rae_check_on.argtypes = [_P, _P]
     lib.rae_build_index.argtypes = [_P, C.c_int64, C.c_int64, _P]
     lib.rae_index_window.argtypes = [_P]
     lib.rae_index_window.restype = C.c_int64
@@ -189,7 +190,7 @@ def load(path: str | None = None):
                "rae_neg_sample", "rae_neg_sample_philox", "rae_plan_create", "rae_plan_destroy", "rae_plan_forms", "rae_set_negatives", "rae_set_cursor",
                "rae_advance_cursor", "rae_step_forward", "rae_step_update", "rae_train_step",
                "rae_step_forward_at", "rae_step_update_at",
-               "rae_check", "rae_label", "rae_build_index"):
+               "rae_check", "rae_check_on", "rae_label", "rae_build_index"):
         getattr(lib, fn).restype = C.c_int
     if path is None:
         _lib = lib

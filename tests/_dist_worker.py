@@ -17,6 +17,8 @@ MODE
              argument 3: the data-parallel update ("replicated" | "partitioned").
   oracle_part  the row-owner partitioned update's protocol on the float64 oracle.
   rows       rae.dist.Exchange.rows / sync_rows / max_int over gloo.
+  gpu_c4dp   BASELINE config 4's model shape (split SP forward + wire records + k_vrec) on a
+             reduced synthetic set; argument 3: the data-parallel update.
   gpu_ckpt   partitioned update, gather() on every rank, then a rank-0-only checkpoint.
   nccl1      one rank over RCCL: the captured exchange == no exchange, bitwise (run_nccl1).
 """
@@ -240,6 +242,48 @@ def run_gpu_c3(out, steps=3, dp_update="replicated", heavy_chunk="auto"):
         np.save(os.path.join(out, f"c3_{k}_{rk}.npy"), v.detach().cpu().numpy())
 
 
+C4DP_SHAPE = dict(N=20_000, d=2 ** 15, ntrue=300, m=300, r=300, s=50, l=100, steps=3, seed=1234)
+
+
+def c4dp_dataset():
+    from rae.data import synthetic_dataset
+    c = C4DP_SHAPE
+    return synthetic_dataset(c["N"], c["d"], c["ntrue"], seed=c["seed"])
+
+
+def run_gpu_c4dp(out, dp_update="replicated"):
+    """BASELINE config 4's model shape (K = 300, embed 300, neg 50, l = 100 per rank) on a
+    reduced synthetic set: the data-parallel kernels the 8-GPU config runs together -- the split
+    SP forward (r m > 32768), the wire records with every example's dw1 / dw2 (dp_dense records
+    at l = 100), k_vrec rebuilding V1 / V2 / G1 after the exchange, 102 record slots (private rows
+    off) -- for the first `steps` global batches of an epoch."""
+    from rae import dist as rdist
+    from rae.inducer import ReconstructInducer
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    c = C4DP_SHAPE
+    data, gold = c4dp_dataset()
+    ex = rdist.make_exchange(ws, rk)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, c["l"], c["r"], c["m"],
+                             c["s"], 0.0, 0.0, "adagrad", "c4dp", "sp", False, True, False, 1.0,
+                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
+                             dp_update=dp_update)
+    ind.compile_function()
+    eng = ind.engine
+    forms = eng.kernel_forms_in_use()
+    want = {"sp_forward": "split", "dp_update": dp_update, "priv_rows": "off", "dp_dense": "records"}
+    assert {k: forms[k] for k in want} == want, forms
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    eng.run(0, c["steps"])
+    torch.cuda.synchronize()
+    eng.check()
+    eng.sync_replicas()
+    params = {k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()}
+    np.savez(os.path.join(out, f"c4dp_{dp_update}_{rk}.npz"),
+             costs=eng.costs[:c["steps"]].cpu().numpy(), **params)
+
+
 def run_gpu_ckpt(out, decoder):
     """Partitioned update, then a rank-0-only checkpoint: every rank calls gather() (the
     collective), then rank 0 alone saves -- which must not start a collective -- and every
@@ -364,6 +408,8 @@ def main():
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
                        heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")
+        elif mode == "gpu_c4dp":
+            run_gpu_c4dp(out, dp_update=dec if dec != "sp" else "replicated")
         elif mode == "gpu_ckpt":
             run_gpu_ckpt(out, dec)
         elif mode == "nccl1":

@@ -108,6 +108,26 @@ def test_shipped_library_is_not_a_diagnostic_build(built_lib):
     for f in _lib.source_files():
         txt = open(f).read()
         assert "getenv" not in txt, f
+    # no knockout / instrumentation define in the product flags or the shipped build's command
+    flags = " ".join(_lib.BUILD_FLAGS)
+    log = os.path.join(ROOT, "relation-autoencoder_amd", "rae", "librae_hip.build.log")
+    cmd = open(log).readline() if os.path.exists(log) else ""
+    for knob in ("RAE_KO_", "RAE_DIAG", "RAE_STAMPS"):
+        assert knob not in flags and knob not in cmd, knob
+
+
+def test_knockout_knobs_refuse_a_product_build(tmp_path):
+    """A timing knockout (-DRAE_KO_*: wrong results) compiles only into a diagnostic build
+    (-DRAE_DIAG); the host-side preprocessing pass of a product build stops at the #error."""
+    import subprocess
+    src = os.path.join(ROOT, "relation-autoencoder_amd", "csrc", "rae.hip")
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-E",
+            "--cuda-host-only", src, "-o", str(tmp_path / "pp.i")]
+    for knob in ("RAE_KO_C", "RAE_KO_W", "RAE_KO_A"):
+        p = subprocess.run(base + [f"-D{knob}=1"], capture_output=True, text=True)
+        assert p.returncode != 0 and "timing knockouts" in p.stderr, (knob, p.stderr[-500:])
+    p = subprocess.run(base + ["-DRAE_KO_C=1", "-DRAE_DIAG"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-500:]
 
 
 def test_plan_create_rejects_unknown_kernel_form(built_lib):

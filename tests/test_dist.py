@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import rae_oracle as O
-from _dist_worker import DP_SHAPE, _dataset
+from _dist_worker import C4DP_SHAPE, DP_SHAPE, _dataset, c4dp_dataset
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "_dist_worker.py")
@@ -185,3 +185,73 @@ def test_rccl_one_rank_captured_exchange(built_lib, cuda_dev, tmp_path):
     replays correctly."""
     _launch(["nccl1", str(tmp_path)], nproc=1, timeout=300)
     assert (tmp_path / "nccl1.ok").exists()
+
+
+_C4DP = {}
+
+
+def _c4dp_reference(cuda_dev, ws):
+    """(float64 oracle costs + params, single-rank HIP run) at the global batch ws * l of the
+    C4-shape data-parallel test, cached per ws.  The single-rank plan runs the same split SP
+    forward with full records (V1 / V2 / G1 written by the forward itself)."""
+    if ws in _C4DP:
+        return _C4DP[ws]
+    import torch
+    from rae.inducer import ReconstructInducer
+    c = C4DP_SHAPE
+    L = ws * c["l"]
+    data, gold = c4dp_dataset()
+    sp_ = data.split["train"]
+    tr = O.OracleTrainer("sp", sp_.xFeats, sp_.args1, sp_.args2, data.negSamplingCum,
+                         np.random.RandomState(2), c["m"], c["r"], c["s"], L, lr=0.1, alpha=1.0)
+    N = sp_.xFeats.shape[0]
+    n1 = O.negative_samples(tr.rng, data.negSamplingCum, N, c["s"])
+    n2 = O.negative_samples(tr.rng, data.negSamplingCum, N, c["s"])
+    costs = np.array([tr.train_batch(b, n1[:, b * L:(b + 1) * L], n2[:, b * L:(b + 1) * L])
+                      for b in range(c["steps"])])
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, L, c["r"], c["m"],
+                             c["s"], 0.0, 0.0, "adagrad", "c4dp1", "sp", False, True, False, 1.0,
+                             device=cuda_dev, graph_chunk=1)
+    ind.compile_function()
+    eng = ind.engine
+    assert eng.kernel_forms_in_use()["sp_forward"] == "split"
+    assert eng.kernel_forms_in_use()["priv_rows"] == "off"
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    eng.run(0, c["steps"])
+    torch.cuda.synchronize()
+    eng.check()
+    single = ({k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()},
+              eng.costs[:c["steps"]].cpu().numpy())
+    ind._drop_engine()
+    _C4DP[ws] = (costs, tr.params, single)
+    return _C4DP[ws]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ws", [2, 4])
+def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
+    """BASELINE config 4's data-parallel kernel combination -- K = 300,
+    embed 300, neg 50, l = 100 per rank: the split SP forward, the wire records (dw1 / dw2 per
+    example), k_vrec and 102 record slots with private rows off -- on `ws` ranks sharing the GPU
+    (gloo), both update forms (the worker asserts the resolved forms).  Checked:
+      * replicas bit-identical, partitioned == replicated bitwise;
+      * == the float64 oracle at the global batch (fp32 tolerance);
+      * == a single-rank plan at the global batch, whose split forward writes V1 / V2 / G1 into
+        the records itself, BITWISE: k_vrec rebuilds exactly the split forward's vectors
+        (k_vrec) and the update sums them in the same order."""
+    _launch(["gpu_c4dp", str(tmp_path), "replicated"], nproc=ws, timeout=600)
+    _launch(["gpu_c4dp", str(tmp_path), "partitioned"], nproc=ws, timeout=600)
+    want_c, want_p, (single_p, single_c) = _c4dp_reference(cuda_dev, ws)
+    gr = [np.load(tmp_path / f"c4dp_replicated_{k}.npz") for k in range(ws)]
+    gp = [np.load(tmp_path / f"c4dp_partitioned_{k}.npz") for k in range(ws)]
+    for g in gr[1:] + gp:
+        np.testing.assert_array_equal(g["costs"], gr[0]["costs"])
+        for k in want_p:
+            np.testing.assert_array_equal(g[k], gr[0][k], err_msg=k)
+    np.testing.assert_allclose(gr[0]["costs"], want_c, rtol=2e-5, atol=2e-5)
+    for k, v in want_p.items():
+        err = np.abs(gr[0][k].astype(np.float64) - v)
+        assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"
+    np.testing.assert_array_equal(gr[0]["costs"], single_c)
+    for k in want_p:
+        np.testing.assert_array_equal(gr[0][k], single_p[k], err_msg=k)
