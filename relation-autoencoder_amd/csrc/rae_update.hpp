@@ -434,8 +434,33 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
     g.zero();
     float gb = 0.f;
-    entity_accum<V4, Q, VS>(a, base, seg.y, seg.z, seg.w, g, gb, lane);
-    gb = wave_sum(gb);
+    if (seg.z - seg.y > RAE_VHEAVY) {
+        // a very heavy row the workgroup slots (NVC) could not take: wg_entity_row's arithmetic
+        // in one wave -- four contiguous quarters summed separately, combined in quarter order
+        // -- so the row's update is bit-identical whichever task runs it (the slots differ
+        // between the replicated and the partitioned data-parallel plans)
+        const int st = seg.y, en = seg.z, ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
+#pragma unroll 1
+        for (int w = 0; w < RAE_NWAVE; ++w) {
+            const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
+            RowVec<V4, Q> gw;
+            gw.zero();
+            float gbw = 0.f;
+            if (c0 < c1) entity_accum<V4, Q, VS>(a, base, c0, c1, seg.w, gw, gbw, lane);
+            gbw = wave_sum(gbw);
+            if (w == 0) {
+                g = gw;
+                gb = gbw;
+            } else {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) vadd(g.v[q], gw.v[q]);
+                gb += gbw;
+            }
+        }
+    } else {
+        entity_accum<V4, Q, VS>(a, base, seg.y, seg.z, seg.w, g, gb, lane);
+        gb = wave_sum(gb);
+    }
     apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
     if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb);
 }
@@ -585,7 +610,26 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
     }
 #endif
     g.zero();
-    feature_accum<V4, Q>(a, ex0, base, seg.y, seg.z, seg.w, g, lane);
+    if (seg.z - seg.y > RAE_VHEAVY) {
+        // an overflowed very heavy row: wg_feature_row's four-quarter arithmetic in one wave
+        // (bit-identical to the workgroup task; see task_entity_row)
+        const int st = seg.y, en = seg.z, ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
+#pragma unroll 1
+        for (int w = 0; w < RAE_NWAVE; ++w) {
+            const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
+            RowVec<V4, Q> gw;
+            gw.zero();
+            if (c0 < c1) feature_accum<V4, Q>(a, ex0, base, c0, c1, seg.w, gw, lane);
+            if (w == 0) {
+                g = gw;
+            } else {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) vadd(g.v[q], gw.v[q]);
+            }
+        }
+    } else {
+        feature_accum<V4, Q>(a, ex0, base, seg.y, seg.z, seg.w, g, lane);
+    }
     feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
 }
 

@@ -44,6 +44,11 @@ for st in "$@"; do
       timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-label-pass > $O/b512.json 2> $O/b512.err \
         || { echo b512 bench failed; tail -30 $O/b512.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/b512.json')); print('b512', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), 'hostq', round(d['timed_region_host_queue_us'],1), {k: round(v, 2) for k, v in d['kernel_us'].items()})" ;;
+    hosttrace)
+      # host time of every call inside the timed region (driver command, timing only)
+      timeout -k 10 300 python3 -u tools/probes/bench_host_trace.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-label-pass > $O/hosttrace.json 2> $O/hosttrace.err \
+        || { echo hosttrace failed; tail -30 $O/hosttrace.err; exit 1; }
+      tail -25 $O/hosttrace.err ;;
     bench)
       timeout -k 10 500 python3 -u bench.py > $O/bench.json 2> $O/bench.err \
         || { echo bench failed; tail -30 $O/bench.err; exit 1; }
