@@ -205,7 +205,7 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
             float* v = vb + (int64_t)bo * a.vbs;
             v[a.vV1 + i] = o1[reg];
             v[a.vV2 + i] = o2[reg];
-            v[a.vG1 + i] = dlv[reg] * o1[reg] + drv[reg] * o2[reg];
+            v[a.vG1 + i] = fmaf(dlv[reg], o1[reg], drv[reg] * o2[reg]);   // as k_sp_dec
         }
     }
 }
@@ -295,7 +295,8 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
         dwr[a.dw1o + i] = S.sdw1[i];
         dwr[a.dw2o + i] = S.sdw2[i];
-        if (!a.lay.wire) rec[a.lay.oG1 + i] = dl * S.swC1[i] + dr * S.swC2[i];   // A[e1]
+        // A[e1]'s vector, one explicit fma (k_vrec forms it the same way: bit-identical)
+        if (!a.lay.wire) rec[a.lay.oG1 + i] = fmaf(dl, S.swC1[i], dr * S.swC2[i]);
     }
     if (a.lay.wire && threadIdx.x == 0) {                 // k_vrec rebuilds G1 from (dl, dr)
         rec[a.lay.oAux + 0] = dl;

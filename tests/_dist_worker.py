@@ -275,13 +275,16 @@ def run_gpu_c4dp(out, dp_update="replicated"):
     want = {"sp_forward": "split", "dp_update": dp_update, "priv_rows": "off", "dp_dense": "records"}
     assert {k: forms[k] for k in want} == want, forms
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
-    eng.run(0, c["steps"])
-    torch.cuda.synchronize()
-    eng.check()
-    eng.sync_replicas()
-    params = {k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()}
+    snap = {}
+    for b in range(c["steps"]):          # one step at a time: the parameters after every step
+        eng.run(b, 1)
+        torch.cuda.synchronize()
+        eng.check()
+        eng.sync_replicas()
+        for k, v in ind.modelFunc.named_params().items():
+            snap[f"{k}@{b}"] = v.detach().cpu().numpy()
     np.savez(os.path.join(out, f"c4dp_{dp_update}_{rk}.npz"),
-             costs=eng.costs[:c["steps"]].cpu().numpy(), **params)
+             costs=eng.costs[:c["steps"]].cpu().numpy(), **snap)
 
 
 def run_gpu_ckpt(out, decoder):
