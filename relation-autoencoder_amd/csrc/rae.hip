@@ -6,7 +6,8 @@
 //   bilinear:  k_bil_enc -> k_bil_mt (MFMA) -> k_bil_dec -> k_bil_mt (MFMA) -> k_bil_dp (MFMA)
 //              -> k_bil_fin
 //                         (rae_bilinear.hpp) -> exchange record
-//   (the per-batch row index is built ahead, a window of batches at a time: k_build_index)
+//   (the per-batch row index is built ahead, a window of batches at a time: k_idx_count ->
+//    k_idx_scatter -> k_idx_sort -> k_build_tasks, rae_index.hpp)
 //   [caller all-gathers the exchange records across data-parallel ranks]
 //   k_update   one wavefront per distinct referenced row / dense decoder row / bias:
 //              deterministic gradient sums + AdaGrad/SGD in place (rae_update.hpp)
@@ -14,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -160,16 +162,33 @@ __global__ __launch_bounds__(RAE_FINT) void k_bil_fin(StepArgs a) {
 typedef FixDims<100, 200, 20> DimsC3;
 typedef FixDims<30, 100, 10> DimsC2;
 
-// row index of global batches [first, first + gridDim.x): blockIdx.y 0 -> A/Ab, 1 -> W
-__global__ __launch_bounds__(RAE_FBT) void k_build_index(StepArgs a, int64_t first) {
+// row index of global batches [first, first + gridDim.x) (rae_index.hpp): blockIdx.y = table
+// (0 A / Ab, 1 W; 2: the example descriptors), blockIdx.z = slice of RAE_IDX_EPS examples or
+// hash partition
+__global__ __launch_bounds__(RAE_BT) void k_idx_count(StepArgs a, int64_t first) {
+    __shared__ int sh[RAE_IDX_HMAX + RAE_IDX_EPS + 1];
+    const int64_t g = first + blockIdx.x;
+    if (blockIdx.y == 2) {
+        build_batch_desc<RAE_BT>(a, g, g % a.index_window, blockIdx.z);
+        return;
+    }
+    index_count<RAE_BT>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, sh);
+}
+__global__ __launch_bounds__(RAE_BT) void k_idx_scatter(StepArgs a, int64_t first) {
+    __shared__ int sh[2 * RAE_IDX_HMAX + RAE_IDX_EPS + 1 + 32];
+    const int64_t g = first + blockIdx.x;
+    index_scatter<RAE_BT>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, sh);
+}
+__global__ __launch_bounds__(RAE_FBT) void k_idx_sort(StepArgs a, int64_t first) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = first + blockIdx.x;
-    if (blockIdx.y == 2) build_batch_desc<RAE_FBT>(a, g, g % a.index_window);
-    else build_batch_index<RAE_FBT>(a, g, g % a.index_window, blockIdx.y == 0, smem);
+    index_sort<RAE_FBT>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, smem);
 }
-// the update's dispatch tables of the same batches (after k_build_index)
+// the update's dispatch tables of the same batches (after k_idx_sort)
 __global__ __launch_bounds__(RAE_BT) void k_build_tasks(StepArgs a, int64_t first) {
-    build_batch_tasks<RAE_BT>(a, (first + blockIdx.x) % a.index_window);
+    __shared__ int sh[6 * (RAE_IDX_HMAX + 1)];
+    const int64_t g = first + blockIdx.x;
+    build_batch_tasks<RAE_BT>(a, g, g % a.index_window, sh);
 }
 
 // partitioned data-parallel update (rae_dp.hpp): the peers' row lists of global batches
@@ -786,6 +805,12 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.HW = index_partitions(a.RW);
     a.G = c.world_size;
     a.part = c.dp_update == RAE_DPUPD_PARTITIONED ? 1 : 0;
+    if (a.HA > RAE_IDX_HMAX || a.HW > RAE_IDX_HMAX) {
+        delete p;
+        return fail(RAE_E_INVALID, "global batch too large for the row index (more than " +
+                                   std::to_string(RAE_IDX_HMAX * RAE_IDX_PART) +
+                                   " records of one table)");
+    }
     {
         const int64_t nb = c.n_examples / L;
         // partitioned: the peers' row lists take 2 G (LA + LW) ints per slot -> a shorter window
@@ -814,14 +839,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     };
     const size_t o_cursor = take(8), o_zero = take(8), o_err = take(8), o_base = take(8);
     const size_t W_ = (size_t)a.index_window;
-    const size_t o_hdrA = take(16 * W_), o_hdrW = take(16 * W_);
     const size_t o_srecA = take(4ull * W_ * a.RA), o_urowA = take(16ull * W_ * a.RA);
     const size_t o_srecW = take(4ull * W_ * a.RW), o_urowW = take(16ull * W_ * a.RW);
-    const size_t o_srowA = a.HA > 1 ? take(4ull * W_ * a.RA) : 0;
-    const size_t o_srowW = a.HW > 1 ? take(4ull * W_ * a.RW) : 0;
+    const size_t o_skeyA = take(8ull * W_ * a.RA), o_skeyW = take(8ull * W_ * a.RW);
+    const size_t o_gidx = take(4ull * W_ * 4 * RAE_IDX_HMAX);
+    const size_t o_pcls = take(16ull * W_ * 2 * RAE_IDX_HMAX);
     a.VCA = a.RA / (RAE_VHEAVY + 1) + 1;       // very heavy rows per batch are fewer than this
     a.VCW = a.RW / (RAE_VHEAVY + 1) + 1;
-    const size_t o_vrowA = take(16ull * W_ * a.VCA), o_vrowW = take(16ull * W_ * a.VCW);
     // the update's dispatch table: every unique row is at most one task (TC = records), and
     // NVC very heavy rows get a workgroup each (L / RAE_NVC_DIV, at least 32 -- the rest run as
     // wave tasks)
@@ -931,17 +955,14 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     p->d_zero = reinterpret_cast<int64_t*>(p->ws + o_zero);
     p->d_err = reinterpret_cast<int*>(p->ws + o_err);
     a.base_cost = reinterpret_cast<float*>(p->ws + o_base);
-    a.hdrA = reinterpret_cast<int32_t*>(p->ws + o_hdrA);
-    a.hdrW = reinterpret_cast<int32_t*>(p->ws + o_hdrW);
     a.srecA = reinterpret_cast<int32_t*>(p->ws + o_srecA);
     a.urowA = reinterpret_cast<int32_t*>(p->ws + o_urowA);
-
     a.srecW = reinterpret_cast<int32_t*>(p->ws + o_srecW);
-    a.srowA = a.HA > 1 ? reinterpret_cast<int32_t*>(p->ws + o_srowA) : nullptr;
-    a.srowW = a.HW > 1 ? reinterpret_cast<int32_t*>(p->ws + o_srowW) : nullptr;
     a.urowW = reinterpret_cast<int32_t*>(p->ws + o_urowW);
-    a.vrowA = reinterpret_cast<int32_t*>(p->ws + o_vrowA);
-    a.vrowW = reinterpret_cast<int32_t*>(p->ws + o_vrowW);
+    a.skeyA = reinterpret_cast<unsigned long long*>(p->ws + o_skeyA);
+    a.skeyW = reinterpret_cast<unsigned long long*>(p->ws + o_skeyW);
+    a.gidx = reinterpret_cast<int32_t*>(p->ws + o_gidx);
+    a.pcls = reinterpret_cast<int32_t*>(p->ws + o_pcls);
     a.thdr = reinterpret_cast<int32_t*>(p->ws + o_thdr);
     a.task = reinterpret_cast<int32_t*>(p->ws + o_task);
     a.vtask = reinterpret_cast<int32_t*>(p->ws + o_vtask);
@@ -969,9 +990,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    // keys, scan scratch, the batch's indptr, segment starts, partition sizes + cursors
-    p->smem_idx = 8ull * RAE_KCAP + 4ull * (32 + L + 1) + 4ull * RAE_KCAP +
-                  8ull * (a.HA > a.HW ? a.HA : a.HW);
+    // k_idx_sort: keys, scan scratch, segment starts
+    p->smem_idx = 8ull * RAE_KCAP + 4ull * 32 + 4ull * RAE_KCAP;
     p->smem_fwd = smem_ex;
     p->smem_spe = p->sp_split ? 4ull * example_smem_floats(0, c.relations, c.embed, 0) : 0;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
@@ -1035,7 +1055,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
             (void)hipFuncSetAttribute((const void*)k_bil_dec<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
         }
-        (void)hipFuncSetAttribute((const void*)k_build_index,
+        (void)hipFuncSetAttribute((const void*)k_idx_sort,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
         (void)hipFuncSetAttribute((const void*)k_build_dplists,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1282,10 +1302,25 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     if (count > p->args.index_window)
         return fail(RAE_E_INVALID, "more batches than the index window holds");
     if (count == 0) return RAE_OK;
-    hipLaunchKernelGGL(k_build_index, dim3((unsigned)count, 3), dim3(RAE_FBT), p->smem_idx, st,
-                       p->args, first);
+    const StepArgs& a = p->args;
+    // the slots' partition counts and scatter cursors start at zero (two ranges when the
+    // window wraps around the ring)
+    {
+        const int64_t s0 = first % a.index_window, n0 = std::min(count, a.index_window - s0);
+        const size_t per = 4ull * 4 * RAE_IDX_HMAX;
+        HIPCHK(hipMemsetAsync(a.gidx + s0 * 4 * RAE_IDX_HMAX, 0, per * n0, st));
+        if (count > n0) HIPCHK(hipMemsetAsync(a.gidx, 0, per * (count - n0), st));
+    }
+    const unsigned nsl = (unsigned)((a.L + RAE_IDX_EPS - 1) / RAE_IDX_EPS);
+    const unsigned hmax = (unsigned)(a.HA > a.HW ? a.HA : a.HW);
+    hipLaunchKernelGGL(k_idx_count, dim3((unsigned)count, 3, nsl), dim3(RAE_BT), 0, st, a, first);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, p->args, first);
+    hipLaunchKernelGGL(k_idx_scatter, dim3((unsigned)count, 2, nsl), dim3(RAE_BT), 0, st, a, first);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_idx_sort, dim3((unsigned)count, 2, hmax), dim3(RAE_FBT), p->smem_idx, st,
+                       a, first);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, a, first);
     HIPCHK(hipGetLastError());
     if (p->args.part) {
         hipLaunchKernelGGL(k_build_dplists, dim3((unsigned)count, p->args.G, 4), dim3(RAE_FBT),

@@ -65,7 +65,10 @@ __device__ void build_dp_list(const StepArgs& a, int64_t g, int64_t slot, int di
     const int NJ = 2 + 2 * a.s;
     const int P0 = tab ? a.indptr[ex0] : 0;
     const int ncand = tab ? a.indptr[ex0 + a.l] - P0 : a.l * NJ;
-    const int H = (ncand + RAE_DPL_KEYS - 1) / RAE_DPL_KEYS;    // hash passes (row / G) % H
+    // hash passes (row / G) % H: sized from the candidates rank y keeps (~1 / G of them, twice
+    // that for the Zipf skew) -- one pass of the scan and sort where ncand / RAE_DPL_KEYS passes
+    // had each re-scanned every candidate
+    const int H = (2 * ((ncand + G - 1) / G) + RAE_DPL_KEYS - 1) / RAE_DPL_KEYS;
     int total = 0;
     for (int h = 0; h < (H > 0 ? H : 1); ++h) {
         if (tid == 0) sint[0] = 0;

@@ -12,24 +12,20 @@
 //
 // The index depends only on the batch's entity ids, negatives and CSR rows -- not on the
 // parameters -- so it is built ahead of the steps, for a window of batches per launch
-// (k_build_index, one workgroup per (batch, A|W)), off the step's critical path.
-// Layout per batch slot (slot = batch % window):
-//   hdr[slot]            = (records, heavy + light rows, heavy rows, very heavy rows)
-//   srec[slot][i]        = record id, i in sorted order
+// (k_idx_count -> k_idx_scatter -> k_idx_sort -> k_build_tasks), off the step's critical path.
+// Layout per batch slot (slot = batch % window), per table (A: entity rows, W: feature rows):
+//   srec[slot][i]        = record id, i in sorted (row, record) order, partition after partition
 //   seg[slot][x]         = (row, first sorted position, end position, first record id) of a
-//                          unique row with at most RAE_VHEAVY records; rows with more than
-//                          RAE_HEAVY ("heavy": the Zipf-frequent entities / features) fill
-//                          x = 0, 1, ... and the light rows fill x = Rcap-1, Rcap-2, ... so the
-//                          update can hand the heavy rows -- its longest one-wave tasks -- to
-//                          the first-dispatched waves, and a one-record row needs no srec read
-//                          (its record rides in the segment)
-//   vseg[slot][x]        = the same for rows with more than RAE_VHEAVY records ("very heavy":
-//                          tens to hundreds of records at a large global batch), which the
-//                          update splits over the four waves of a workgroup
+//                          distinct row, at its partition's offset in class order: heavy (more
+//                          than RAE_HEAVY records: the Zipf-frequent entities / features), light,
+//                          very heavy (more than RAE_VHEAVY: split over a workgroup's four waves
+//                          by the update); a one-record row needs no srec read (its record rides
+//                          in the segment)
+//   pcls[slot][p]        = (heavy, light, very heavy rows, offset) of partition p
 // Records: A-index rec = b*NJ + j (j = 0 e1, 1 e2, 2+t neg1[t], 2+s+t neg2[t]);
 //          W-index rec = b << posbits | position of the feature in row b.
-// Rows are hash-partitioned (row % H) when a batch has more records than one LDS sort
-// holds; partitions are processed one after another by the same workgroup.
+// Rows are hash-partitioned (row % H, ~RAE_IDX_PART records per partition) so one LDS sort
+// holds a partition; every partition is sorted by its own workgroup (k_idx_sort).
 #pragma once
 #include "rae_common.hpp"
 #include "rae_step.hpp"
@@ -54,6 +50,30 @@ __device__ __forceinline__ int block_flag_scan(int flag, int* ws, int* total) {
     }
     *total = tot;
     return off + pre;
+}
+
+// exclusive block-wide prefix sum of one int per thread (fixed order), and the block total
+template <int BT>
+__device__ __forceinline__ int block_int_scan(int v, int* ws, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < BT / 64; ++i) {
+        const int c = ws[i];
+        off += (i < w) ? c : 0;
+        tot += c;
+    }
+    *total = tot;
+    return off + incl - v;
 }
 
 // Bitonic sort of n2 (a power of two) 64-bit keys in LDS: one compare-exchange pair (i, i + j)
@@ -83,278 +103,363 @@ __device__ void lds_bitonic_sort(unsigned long long* keys, int n2) {
 #ifndef RAE_IDX_PART
 #define RAE_IDX_PART 1024      // measured at C3: 4096 -> 0.98, 2048 -> 0.83, 1024 -> 0.79 us per batch
 #endif
+#define RAE_IDX_HMAX 1024      // partitions per batch and table (k_build_tasks' LDS prefix tables)
+#define RAE_IDX_EPS 32         // examples per slice of the binning launches
 __host__ __device__ inline int index_partitions(int nrec) {
     return nrec <= RAE_IDX_PART ? 1 : (nrec + RAE_IDX_PART - 1) / RAE_IDX_PART;
 }
 
-template <int BT>
-__device__ void build_batch_index(const StepArgs& a, int64_t g, int64_t slot, bool isA,
-                                  char* smem) {
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-    int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);   // [0] count, [1..24] scan scratch
-    int* sptr = sint + 32;                                   // batch indptr (W index)
-    int* sstart = sptr + a.L + 1;                            // segment starts of a partition
-    const int tid = threadIdx.x;
+// ---- the row index, built in four launches per window of batches ---------------------------
+//   k_idx_count    (batch, table, slice of RAE_IDX_EPS examples): the slice's kept records per
+//                  hash partition, added into the slot's partition counts (gidx[.][0])
+//   k_idx_scatter  (batch, table, slice): the partitions' offsets (exclusive prefix of the
+//                  counts), a block per (slice, partition) reserved from the scatter cursors
+//                  (gidx[.][1]), the slice's (row, record) keys written there -- binned by
+//                  partition, in no particular order inside a partition
+//   k_idx_sort     (batch, table, partition): the partition's keys sorted in LDS -> the sorted
+//                  record ids (srec, at the partition's offset) and its segments -- one per
+//                  distinct row: (row, first position, end position, first record id) --
+//                  class-ordered at the same offset: heavy (> RAE_HEAVY records), light, very
+//                  heavy (> RAE_VHEAVY); private rows (one record, StepArgs::priv) set their
+//                  example's mask bit instead; the class counts per partition (pcls)
+//   k_build_tasks  (batch): the update's dispatch table from the partitions' class lists
+// Every launch's work is spread over (batch x partition) workgroups -- the whole GPU at a
+// data-parallel global batch, where one workgroup per batch and table had sorted every
+// partition in turn (28.9 / 65.4 us per batch at G = 8, l = 1024).  Keys are unique
+// (row, record) pairs, so the sorted order -- and everything built from it -- is independent of
+// the scatter's arbitrary order.
+struct IdxTab {
+    int nrec, H;                 // records of the table in the batch, hash partitions
+    int Rcap;
+    int32_t* srec;
+    int4* seg;
+    unsigned long long* skey;
+};
+__device__ __forceinline__ IdxTab idx_tab(const StepArgs& a, int64_t g, int64_t slot, int tab) {
+    IdxTab t;
     const int64_t ex0 = g * (int64_t)a.L;
-    const int NJ = 2 + 2 * a.s;
-    const int Rcap = isA ? a.RA : a.RW;
-    int32_t* hdr = (isA ? a.hdrA : a.hdrW) + 4 * slot;
-    int32_t* srec = (isA ? a.srecA : a.srecW) + slot * (int64_t)Rcap;
-    int4* seg = reinterpret_cast<int4*>(isA ? a.urowA : a.urowW) + slot * (int64_t)Rcap;
-    const int Vcap = isA ? a.VCA : a.VCW;
-    int4* vseg = reinterpret_cast<int4*>(isA ? a.vrowA : a.vrowW) + slot * (int64_t)Vcap;
-    if (!isA)
-        for (int b = tid; b <= a.L; b += BT) sptr[b] = a.indptr[ex0 + b];
-    if (a.priv) {                // private-row masks of this batch: A words 0, 1 / W words 2, 3
-        int2* pm = reinterpret_cast<int2*>(a.pmask + slot * (int64_t)a.L * 4) + (isA ? 0 : 1);
-        for (int b = tid; b < a.L; b += BT) pm[2 * b] = make_int2(0, 0);
-    }
-    __syncthreads();
-    const int P0 = isA ? 0 : sptr[0];
-    const int nrec = isA ? a.L * NJ : sptr[a.L] - P0;
-    if (nrec > Rcap) {
-        if (tid == 0) {
-            atomicOr(a.err, 4);
-            hdr[0] = hdr[1] = hdr[2] = hdr[3] = 0;
-        }
-        return;
-    }
-    // partitioned data-parallel update: this rank keeps only the rows it owns (row % G == rank),
-    // ~nrec / G records, so it sizes its partitions from that share and hashes on row / G (row %
-    // H would leave whole partitions empty when gcd(G, H) > 1)
-    const int H = index_partitions(a.part ? (nrec + a.G - 1) / a.G : nrec);
-    // record at position idx of the batch: its parameter row (and, want_rec, its record id)
-    auto rec_at = [&](int idx, int& row, unsigned& rec, bool want_rec) {
-        if (isA) {
-            const int j = idx / a.L, b = idx - j * a.L;          // j-major: coalesced columns
+    t.nrec = tab ? a.indptr[ex0 + a.L] - a.indptr[ex0] : a.L * (2 + 2 * a.s);
+    t.H = index_partitions(a.part ? (t.nrec + a.G - 1) / a.G : t.nrec);
+    t.Rcap = tab ? a.RW : a.RA;
+    t.srec = (tab ? a.srecW : a.srecA) + slot * (int64_t)t.Rcap;
+    t.seg = reinterpret_cast<int4*>(tab ? a.urowW : a.urowA) + slot * (int64_t)t.Rcap;
+    t.skey = (tab ? a.skeyW : a.skeyA) + slot * (int64_t)t.Rcap;
+    return t;
+}
+// the slot's partition counts (which 0) / scatter cursors (which 1) of a table
+__device__ __forceinline__ int32_t* idx_gc(const StepArgs& a, int64_t slot, int tab, int which) {
+    return a.gidx + ((slot * 2 + tab) * 2 + which) * RAE_IDX_HMAX;
+}
+__device__ __forceinline__ int4* idx_cls(const StepArgs& a, int64_t slot, int tab) {
+    return reinterpret_cast<int4*>(a.pcls) + (slot * 2 + tab) * RAE_IDX_HMAX;
+}
+// partitioned data-parallel update: this rank keeps only the rows it owns (row % G == rank) and
+// hashes on row / G (row % H would leave whole partitions empty when gcd(G, H) > 1)
+__device__ __forceinline__ bool idx_keep(const StepArgs& a, int row) { return !a.part || row % a.G == a.rank; }
+__device__ __forceinline__ int idx_part(const StepArgs& a, int row, int H) {
+    return (a.part ? row / a.G : row) % H;
+}
+
+// The records of the examples [b0, b1) of global batch g: f(row, record id).
+// A-index record = b * NJ + j (j = 0 e1, 1 e2, 2+t neg1[t], 2+s+t neg2[t]), enumerated j-major
+// (coalesced columns); W-index record = b << posbits | position of the feature in row b.
+template <int BT, class F>
+__device__ __forceinline__ void idx_slice_records(const StepArgs& a, int64_t g, int tab, int b0,
+                                                  int b1, int* sptr, F&& f) {
+    const int tid = threadIdx.x, nb = b1 - b0;
+    const int64_t ex0 = g * (int64_t)a.L;
+    if (tab == 0) {
+        const int NJ = 2 + 2 * a.s;
+        for (int idx = tid; idx < NJ * nb; idx += BT) {
+            const int j = idx / nb, b = b0 + (idx - j * nb);
             const int64_t ex = ex0 + b;
             const int64_t col = a.neg_mode ? ex : (int64_t)b;
+            int row;
             if (j == 0) row = a.args1[ex];
             else if (j == 1) row = a.args2[ex];
             else if (j < 2 + a.s) row = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
             else row = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
-            rec = (unsigned)(b * NJ + j);
-        } else {
-            row = a.indices[P0 + idx];
-            rec = 0;
-            if (want_rec) {
-                int lo = 0, hi = a.L - 1;                               // example of position idx
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sptr[mid] - P0 <= idx) lo = mid; else hi = mid - 1;
-                }
-                rec = ((unsigned)lo << a.posbits) | (unsigned)(idx - (sptr[lo] - P0));
-            }
+            f(row, (unsigned)(b * NJ + j));
         }
-    };
-    // partitioned data-parallel update: this rank's update visits only the rows it owns (rae_dp.hpp)
-    auto keep = [&](int row) { return !a.part || row % a.G == a.rank; };
-    auto part_of = [&](int row) { return (a.part ? row / a.G : row) % H; };
-    // More than one partition: the records are binned by partition in ONE pass (an LDS
-    // histogram, its prefix sums, a scatter of (row, record) into the slot's srow / srec at the
-    // partition's final position -- partition h's sorted records end up in the same range), so
-    // the work is two scans of the batch instead of one scan per partition (H ~ records / 1024:
-    // 33 scans of 34 k records per batch at L = 800).
-    int* hcnt = sstart + RAE_KCAP;                           // H partition sizes
-    int* hcur = hcnt + H;                                    // H scatter cursors
-    int32_t* srow = (isA ? a.srowA : a.srowW) + slot * (int64_t)Rcap;
-    if (H > 1) {
-        for (int h = tid; h < H; h += BT) hcnt[h] = 0;
-        __syncthreads();
-        for (int idx = tid; idx < nrec; idx += BT) {
-            int row;
-            unsigned rec;
-            rec_at(idx, row, rec, false);
-            if (keep(row)) atomicAdd(&hcnt[part_of(row)], 1);
-        }
-        __syncthreads();
-        if (tid < RAE_WAVE) {                                // exclusive prefix sum, wave 0
-            const int per = (H + RAE_WAVE - 1) / RAE_WAVE, h0 = tid * per;
-            int sum = 0;
-            for (int h = h0; h < H && h < h0 + per; ++h) sum += hcnt[h];
-            int incl = sum;
-            for (int o = 1; o < RAE_WAVE; o <<= 1) {
-                const int t = __shfl_up(incl, o, RAE_WAVE);
-                if (tid >= o) incl += t;
+    } else {
+        // the slice's CSR row starts in LDS (sptr: nb + 1 ints), a position's example by
+        // binary search there
+        const int P0 = sptr[0], n = sptr[nb] - P0;
+        for (int idx = tid; idx < n; idx += BT) {
+            int lo = 0, hi = nb - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (sptr[mid] - P0 <= idx) lo = mid; else hi = mid - 1;
             }
-            int ex = incl - sum;
-            for (int h = h0; h < H && h < h0 + per; ++h) {
-                hcur[h] = ex;
-                ex += hcnt[h];
-            }
+            const int pos = P0 + idx;
+            f(a.indices[pos], ((unsigned)(b0 + lo) << a.posbits) | (unsigned)(pos - sptr[lo]));
         }
-        __syncthreads();
-        for (int idx = tid; idx < nrec; idx += BT) {
-            int row;
-            unsigned rec;
-            rec_at(idx, row, rec, true);
-            if (keep(row)) {
-                const int pos = atomicAdd(&hcur[part_of(row)], 1);
-                srow[pos] = row;
-                srec[pos] = (int32_t)rec;
-            }
-        }
-        __syncthreads();
     }
-    int base_i = 0, nh = 0, nl = 0, nv = 0;
-    for (int h = 0; h < H; ++h) {
-        if (H > 1) {
-            // partition h: its binned records (base == base_i: bins in partition order)
-            const int cnt_h = hcnt[h];
-            if (tid == 0) sint[0] = cnt_h;
-            for (int i = tid; i < cnt_h && i < RAE_KCAP; i += BT)
-                keys[i] = ((unsigned long long)(unsigned)srow[base_i + i] << 32) |
-                          (unsigned)srec[base_i + i];
-        } else {
-            if (tid == 0) sint[0] = 0;
-            __syncthreads();
-            for (int idx = tid; idx < nrec; idx += BT) {
-                int row;
-                unsigned rec;
-                rec_at(idx, row, rec, true);
-                if (keep(row)) {
-                    const int sl = atomicAdd(&sint[0], 1);
-                    if (sl < RAE_KCAP) keys[sl] = ((unsigned long long)(unsigned)row << 32) | rec;
-                }
-            }
+}
+
+// k_idx_count: also zeroes the slice's private-row mask words of this table
+template <int BT>
+__device__ void index_count(const StepArgs& a, int64_t g, int64_t slot, int tab, int z, int* sh) {
+    const int tid = threadIdx.x;
+    const int b0 = z * RAE_IDX_EPS;
+    if (b0 >= a.L) return;
+    const int b1 = min(b0 + RAE_IDX_EPS, a.L);
+    const IdxTab t = idx_tab(a, g, slot, tab);
+    int* hist = sh;
+    int* sptr = sh + RAE_IDX_HMAX;
+    if (t.H > RAE_IDX_HMAX || t.nrec > t.Rcap) {
+        if (tid == 0) atomicOr(a.err, tab ? 2 : 1);
+        return;
+    }
+    for (int h = tid; h < t.H; h += BT) hist[h] = 0;
+    if (tab) {
+        const int64_t ex0 = g * (int64_t)a.L;
+        for (int b = tid; b <= b1 - b0; b += BT) sptr[b] = a.indptr[ex0 + b0 + b];
+    }
+    if (a.priv) {
+        int2* pm = reinterpret_cast<int2*>(a.pmask + slot * (int64_t)a.L * 4) + tab;
+        for (int b = b0 + tid; b < b1; b += BT) pm[2 * b] = make_int2(0, 0);
+    }
+    __syncthreads();
+    idx_slice_records<BT>(a, g, tab, b0, b1, sptr, [&](int row, unsigned) {
+        if (idx_keep(a, row)) atomicAdd(&hist[idx_part(a, row, t.H)], 1);
+    });
+    __syncthreads();
+    int32_t* gc = idx_gc(a, slot, tab, 0);
+    for (int h = tid; h < t.H; h += BT)
+        if (hist[h]) atomicAdd(&gc[h], hist[h]);
+}
+
+// exclusive prefix sum over n <= RAE_IDX_HMAX ints of LDS `v` in place (BT threads)
+template <int BT>
+__device__ __forceinline__ void lds_exclusive_scan(int* v, int n, int* ws) {
+    constexpr int PER = (RAE_IDX_HMAX + BT - 1) / BT;
+    const int tid = threadIdx.x, h0 = tid * PER;
+    int x[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        x[k] = h0 + k < n ? v[h0 + k] : 0;
+        sum += x[k];
+    }
+    int tot;
+    int ex = block_int_scan<BT>(sum, ws, &tot);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (h0 + k < n) v[h0 + k] = ex;
+        ex += x[k];
+    }
+    __syncthreads();
+}
+
+template <int BT>
+__device__ void index_scatter(const StepArgs& a, int64_t g, int64_t slot, int tab, int z, int* sh) {
+    const int tid = threadIdx.x;
+    const int b0 = z * RAE_IDX_EPS;
+    if (b0 >= a.L) return;
+    const int b1 = min(b0 + RAE_IDX_EPS, a.L);
+    const IdxTab t = idx_tab(a, g, slot, tab);
+    if (t.H > RAE_IDX_HMAX || t.nrec > t.Rcap) return;         // k_idx_count flagged it
+    int* pre = sh;                                   // partition offsets
+    int* cur = sh + RAE_IDX_HMAX;                    // this slice's block cursors
+    int* sptr = sh + 2 * RAE_IDX_HMAX;
+    int* ws = sptr + RAE_IDX_EPS + 1;
+    const int32_t* gc = idx_gc(a, slot, tab, 0);
+    for (int h = tid; h < t.H; h += BT) {
+        pre[h] = gc[h];
+        cur[h] = 0;
+    }
+    if (tab) {
+        const int64_t ex0 = g * (int64_t)a.L;
+        for (int b = tid; b <= b1 - b0; b += BT) sptr[b] = a.indptr[ex0 + b0 + b];
+    }
+    __syncthreads();
+    lds_exclusive_scan<BT>(pre, t.H, ws);
+    idx_slice_records<BT>(a, g, tab, b0, b1, sptr, [&](int row, unsigned) {
+        if (idx_keep(a, row)) atomicAdd(&cur[idx_part(a, row, t.H)], 1);
+    });
+    __syncthreads();
+    int32_t* gcur = idx_gc(a, slot, tab, 1);
+    for (int h = tid; h < t.H; h += BT)
+        if (cur[h]) cur[h] = pre[h] + atomicAdd(&gcur[h], cur[h]);
+    __syncthreads();
+    idx_slice_records<BT>(a, g, tab, b0, b1, sptr, [&](int row, unsigned rec) {
+        if (idx_keep(a, row)) {
+            const int pos = atomicAdd(&cur[idx_part(a, row, t.H)], 1);
+            t.skey[pos] = ((unsigned long long)(unsigned)row << 32) | rec;
         }
-        __syncthreads();
-        const int cnt = sint[0];
-        if (cnt > RAE_KCAP) {
-            if (tid == 0) {
-                atomicOr(a.err, isA ? 1 : 2);
-                hdr[0] = hdr[1] = hdr[2] = hdr[3] = 0;
-            }
-            return;
+    });
+}
+
+// k_idx_sort: partition h of a table
+template <int BT>
+__device__ void index_sort(const StepArgs& a, int64_t g, int64_t slot, int tab, int h, char* smem) {
+    const int tid = threadIdx.x;
+    const IdxTab t = idx_tab(a, g, slot, tab);
+    if (h >= t.H || t.H > RAE_IDX_HMAX || t.nrec > t.Rcap) return;
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+    int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);    // [0..31] scan scratch
+    int* sstart = sint + 32;                                 // segment starts (<= RAE_KCAP)
+    const int32_t* gc = idx_gc(a, slot, tab, 0);
+    // the partition's offset: the counts of partitions 0..h-1
+    int part = 0;
+    for (int k = tid; k < h; k += BT) part += gc[k];
+    int base;
+    block_int_scan<BT>(part, sint, &base);
+    const int cnt = gc[h];
+    int4* cls = idx_cls(a, slot, tab);
+    if (cnt > RAE_KCAP) {
+        if (tid == 0) {
+            atomicOr(a.err, tab ? 2 : 1);
+            cls[h] = make_int4(0, 0, 0, base);
         }
-        int n2 = 1;
-        while (n2 < cnt) n2 <<= 1;
-        for (int i = cnt + tid; i < n2; i += BT) keys[i] = ~0ull;
-        __syncthreads();
-        lds_bitonic_sort<BT>(keys, n2);
-        // segment heads in sorted order -> sstart[local segment]
-        int nu = 0;
-        for (int i0 = 0; i0 < cnt; i0 += BT) {
-            const int i = i0 + tid;
-            int head = 0;
-            if (i < cnt) {
-                const unsigned long long k = keys[i];
-                const unsigned row = (unsigned)(k >> 32);
-                head = (i == 0) || ((unsigned)(keys[i - 1] >> 32) != row);
-                srec[base_i + i] = (int32_t)(unsigned)(k & 0xffffffffull);
-            }
-            int tot;
-            const int u = nu + block_flag_scan<BT>(head, sint + 1, &tot);
-            if (head) sstart[u] = i;
-            nu += tot;
+        return;
+    }
+    for (int i = tid; i < cnt; i += BT) keys[i] = t.skey[base + i];
+    int n2 = 1;
+    while (n2 < cnt) n2 <<= 1;
+    for (int i = cnt + tid; i < n2; i += BT) keys[i] = ~0ull;
+    __syncthreads();
+    lds_bitonic_sort<BT>(keys, n2);
+    // segment heads in sorted order -> sstart[segment]
+    int nu = 0;
+    for (int i0 = 0; i0 < cnt; i0 += BT) {
+        const int i = i0 + tid;
+        int head = 0;
+        if (i < cnt) {
+            const unsigned long long k = keys[i];
+            head = (i == 0) || ((unsigned)(keys[i - 1] >> 32) != (unsigned)(k >> 32));
+            t.srec[base + i] = (int32_t)(unsigned)(k & 0xffffffffull);
         }
-        __syncthreads();
-        // segments -> very heavy rows to vseg, heavy rows at the front of seg, light rows at
-        // its back (order kept in each class)
-        for (int v0 = 0; v0 < nu; v0 += BT) {
-            const int v = v0 + tid;
-            const bool valid = v < nu;
-            int st = 0, en = 0;
-            if (valid) {
-                st = sstart[v];
-                en = (v + 1 < nu) ? sstart[v + 1] : cnt;
-            }
-            // private row (StepArgs::priv): one record, of an example whose features the
-            // descriptor holds (at most privnf) -- the update's per-example workgroups take it
-            // (SP: e2's rows, with no A gradient, stay in the table)
-            bool psg = false;
-            if (a.priv && valid && en - st == 1) {
-                const unsigned rec = (unsigned)(keys[st] & 0xffffffffull);
-                if (isA) {
-                    const int b = (int)(rec / (unsigned)NJ), j = (int)rec - b * NJ;
-                    psg = (j != 1 || a.dec != 0) && a.indptr[ex0 + b + 1] - a.indptr[ex0 + b] <= a.privnf;
-                    if (psg) atomicOr(a.pmask + (slot * a.L + b) * 4 + (j >> 5), 1 << (j & 31));
-                } else {
-                    const int b = (int)(rec >> a.posbits);
-                    const int pos = (int)(rec & ((1u << a.posbits) - 1u));
-                    psg = sptr[b + 1] - sptr[b] <= a.privnf;
-                    if (psg) atomicOr(a.pmask + (slot * a.L + b) * 4 + 2, 1 << pos);
-                }
+        int tot;
+        const int u = nu + block_flag_scan<BT>(head, sint + 1, &tot);
+        if (head) sstart[u] = i;
+        nu += tot;
+    }
+    __syncthreads();
+    const int64_t ex0 = g * (int64_t)a.L;
+    const int NJ = 2 + 2 * a.s;
+    // segment v's class: 0 heavy, 1 light, 2 very heavy, 3 private (mask bit set, no task)
+    auto seg_class = [&](int v, int& st, int& en, bool mark) {
+        st = sstart[v];
+        en = (v + 1 < nu) ? sstart[v + 1] : cnt;
+        // private row (StepArgs::priv): one record, of an example whose features the
+        // descriptor holds (at most privnf) -- the update's per-example workgroups take it
+        // (SP: e2's rows, with no A gradient, stay in the table)
+        if (a.priv && en - st == 1) {
+            const unsigned rec = (unsigned)(keys[st] & 0xffffffffull);
+            bool psg;
+            if (tab == 0) {
+                const int b = (int)(rec / (unsigned)NJ), j = (int)rec - b * NJ;
+                psg = (j != 1 || a.dec != 0) && a.indptr[ex0 + b + 1] - a.indptr[ex0 + b] <= a.privnf;
+                if (psg && mark) atomicOr(a.pmask + (slot * a.L + b) * 4 + (j >> 5), 1 << (j & 31));
+            } else {
+                const int b = (int)(rec >> a.posbits);
+                const int pos = (int)(rec & ((1u << a.posbits) - 1u));
+                psg = a.indptr[ex0 + b + 1] - a.indptr[ex0 + b] <= a.privnf;
+                if (psg && mark) atomicOr(a.pmask + (slot * a.L + b) * 4 + 2, 1 << pos);
             }
 #ifdef RAE_DIAG_NOSINGLE      // timing knockout (wrong results): rows with one record are skipped
-            psg = psg || (valid && en - st == 1);
+            psg = true;
 #endif
-            const bool vheavy = valid && (en - st) > RAE_VHEAVY;
-            const bool heavy = valid && !vheavy && (en - st) > RAE_HEAVY;
-            int htot, ltot, vtot;
-            const int hp = block_flag_scan<BT>(heavy, sint + 1, &htot);
-            const int lp = block_flag_scan<BT>(valid && !psg && (en - st) <= RAE_HEAVY, sint + 12, &ltot);
-            const int vp = block_flag_scan<BT>(vheavy, sint + 21, &vtot);
-            if (valid) {
-                const unsigned long long k = keys[st];
-                const int4 sg = make_int4((int)(unsigned)(k >> 32), base_i + st, base_i + en,
-                                          (int)(unsigned)(k & 0xffffffffull));
-                if (vheavy) vseg[nv + vp] = sg;
-                else if (!psg) seg[heavy ? nh + hp : Rcap - 1 - (nl + lp)] = sg;
-            }
-            nh += htot;
-            nl += ltot;
-            nv += vtot;
+            if (psg) return 3;
         }
-        base_i += cnt;
-        __syncthreads();
+#ifdef RAE_DIAG_NOSINGLE
+        if (en - st == 1) return 3;
+#endif
+        return (en - st) > RAE_VHEAVY ? 2 : ((en - st) > RAE_HEAVY ? 0 : 1);
+    };
+    // pass 1: class counts; pass 2: every segment at its class position (order kept per class)
+    int n[3] = {0, 0, 0};
+    for (int v0 = 0; v0 < nu; v0 += BT) {
+        const int v = v0 + tid;
+        int st, en, c = -1;
+        if (v < nu) c = seg_class(v, st, en, false);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            int tot;
+            block_flag_scan<BT>(c == k, sint + 1, &tot);
+            n[k] += tot;
+        }
     }
-    if (tid == 0) {
-        hdr[0] = base_i;
-        hdr[1] = nh + nl;
-        hdr[2] = nh;
-        hdr[3] = nv;
+    int o[3] = {0, n[0], n[0] + n[1]};
+    for (int v0 = 0; v0 < nu; v0 += BT) {
+        const int v = v0 + tid;
+        int st = 0, en = 0, c = -1;
+        if (v < nu) c = seg_class(v, st, en, true);
+        int pos = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            int tot;
+            const int p = block_flag_scan<BT>(c == k, sint + 1, &tot);
+            if (c == k) pos = o[k] + p;
+            o[k] += tot;
+        }
+        if (c >= 0 && c < 3) {
+            const unsigned long long k = keys[st];
+            t.seg[base + pos] = make_int4((int)(unsigned)(k >> 32), base + st, base + en,
+                                          (int)(unsigned)(k & 0xffffffffull));
+        }
     }
+    if (tid == 0) cls[h] = make_int4(n[0], n[1], n[2], base);
 }
 
-// The update's dispatch table of a slot, built once the A and W indexes of the batch exist
-// (a second launch): the update's row waves then find their task with ONE load issued at wave
-// start in parallel with the table header, instead of header -> (class counts) -> segment.
+// The update's dispatch table of a slot, built once every partition of the batch is sorted:
+// the update's row waves then find their task with ONE load issued at wave start in parallel
+// with the table header.
 //   vtask[slot][v]  very heavy rows (A first, then W), v < NVC: one workgroup each
 //   task[slot][t]   wave tasks in dispatch order: very heavy rows beyond NVC, heavy A, heavy W,
-//                   light A, light W (the order the update used to derive from the header)
-//   thdr[slot]      (wave tasks, workgroup tasks, 0, 0)
+//                   light A, light W
+//   thdr[slot]      (wave tasks, workgroup tasks, chunked rows, 0)
 // W rows are stored as ~row (negative), A rows as row.
-// exclusive block-wide prefix sum of one int per thread (fixed order), and the block total
+// LDS: for each table and class (heavy, light, very heavy) the exclusive prefix of the
+// partitions' class counts (RAE_IDX_HMAX + 1 ints each); an entry's partition is found by
+// binary search there.
 template <int BT>
-__device__ __forceinline__ int block_int_scan(int v, int* ws, int* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    __syncthreads();
-    if (lane == 63) ws[w] = incl;
-    __syncthreads();
-    int off = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < BT / 64; ++i) {
-        const int c = ws[i];
-        off += (i < w) ? c : 0;
-        tot += c;
-    }
-    *total = tot;
-    return off + incl - v;
-}
-
-template <int BT>
-__device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
+__device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, int* sh) {
     __shared__ int sws[BT / 64];
-    const int4 hA = reinterpret_cast<const int4*>(a.hdrA)[slot];
-    const int4 hW = reinterpret_cast<const int4*>(a.hdrW)[slot];
-    const int HA = hA.z, HW = hW.z, LA = hA.y - hA.z, VA = hA.w, VW = hW.w;
-    int4* vt = reinterpret_cast<int4*>(a.vtask) + slot * a.NVC;
-    int4* tk = reinterpret_cast<int4*>(a.task) + slot * a.TC;
-    const int4* urA = reinterpret_cast<const int4*>(a.urowA) + slot * a.RA;
-    const int4* urW = reinterpret_cast<const int4*>(a.urowW) + slot * a.RW;
-    auto vrow = [&](int v) {
-        int4 sg = v < VA ? reinterpret_cast<const int4*>(a.vrowA)[slot * a.VCA + v]
-                         : reinterpret_cast<const int4*>(a.vrowW)[slot * a.VCW + v - VA];
-        if (v >= VA) sg.x = ~sg.x;
+    int Ht[2];
+    const int4* clsT[2] = {idx_cls(a, slot, 0), idx_cls(a, slot, 1)};
+    int tot[2][3];
+    for (int tab = 0; tab < 2; ++tab) {
+        Ht[tab] = idx_tab(a, g, slot, tab).H;
+        if (Ht[tab] > RAE_IDX_HMAX) Ht[tab] = 0;           // flagged by k_idx_count
+        for (int c = 0; c < 3; ++c) {
+            int* pf = sh + (tab * 3 + c) * (RAE_IDX_HMAX + 1);
+            for (int h = threadIdx.x; h < Ht[tab]; h += BT) {
+                const int4 q = clsT[tab][h];
+                pf[h] = c == 0 ? q.x : (c == 1 ? q.y : q.z);
+            }
+            __syncthreads();
+            int x = 0;
+            for (int h = threadIdx.x; h < Ht[tab]; h += BT) x += pf[h];
+            int t_;
+            block_int_scan<BT>(x, sws, &t_);
+            tot[tab][c] = t_;
+            if (threadIdx.x == 0) pf[Ht[tab]] = t_;
+            lds_exclusive_scan<BT>(pf, Ht[tab], sws);
+        }
+    }
+    // entry x of class c of table tab -> its segment
+    auto seg_of = [&](int tab, int c, int x) {
+        const int* pf = sh + (tab * 3 + c) * (RAE_IDX_HMAX + 1);
+        int lo = 0, hi = Ht[tab] - 1;                      // last partition with pf[h] <= x
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pf[mid] <= x) lo = mid; else hi = mid - 1;
+        }
+        const int4 q = clsT[tab][lo];
+        const int off = c == 0 ? 0 : (c == 1 ? q.x : q.x + q.y);
+        int4 sg = reinterpret_cast<const int4*>(tab ? a.urowW : a.urowA)[slot * (int64_t)(tab ? a.RW : a.RA) +
+                                                                          q.w + off + (x - pf[lo])];
+        if (tab) sg.x = ~sg.x;
         return sg;
     };
+    const int VA = tot[0][2], VW = tot[1][2];
+    const int HA = tot[0][0], HW = tot[1][0], LA = tot[0][1], LW = tot[1][1];
+    int4* vt = reinterpret_cast<int4*>(a.vtask) + slot * a.NVC;
+    int4* tk = reinterpret_cast<int4*>(a.task) + slot * a.TC;
+    auto vrow = [&](int v) { return v < VA ? seg_of(0, 2, v) : seg_of(1, 2, v - VA); };
     // very heavy rows: rows with at least 2 hch records become floor(records / hch) chunk tasks
     // (the first vtask entries; chunk k = records [st + k hch, st + (k+1) hch), the last one
     // to the row's end: hch .. 2 hch - 1 records) plus a combine entry; the others keep one
@@ -404,14 +509,14 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
         NU += tu;
     }
     const int NV = min(NC + NU, a.NVC), XV = NC + NU - NV;
-    const int T = XV + hA.y + hW.y;
+    const int T = XV + HA + HW + LA + LW;
     for (int t = threadIdx.x; t < T - XV; t += BT) {
         int x = t;
         int4 sg;
-        if (x < HA) sg = urA[x];
-        else if ((x -= HA) < HW) { sg = urW[x]; sg.x = ~sg.x; }
-        else if ((x -= HW) < LA) sg = urA[a.RA - 1 - x];
-        else { sg = urW[a.RW - 1 - (x - LA)]; sg.x = ~sg.x; }
+        if (x < HA) sg = seg_of(0, 0, x);
+        else if ((x -= HA) < HW) sg = seg_of(1, 0, x);
+        else if ((x -= HW) < LA) sg = seg_of(0, 1, x);
+        else sg = seg_of(1, 1, x - LA);
         tk[XV + t] = sg;
     }
     if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(T, NV, NF, 0);
@@ -423,12 +528,14 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t slot) {
 // the dependent indptr -> indices -> W-row chain (parameter independent, so built ahead).
 // With the update's private-row tasks on several ranks (dnx == L) every example of the global
 // batch gets one (each rank's update applies all examples' private rows, or its owned ones).
+// (descriptor examples [z RAE_IDX_EPS, (z + 1) RAE_IDX_EPS) of the slot: one slice)
 template <int BT>
-__device__ void build_batch_desc(const StepArgs& a, int64_t g, int64_t slot) {
+__device__ void build_batch_desc(const StepArgs& a, int64_t g, int64_t slot, int z) {
     const int NJ = 2 + 2 * a.s, DS = a.dstride;
     int32_t* out = a.desc + slot * (int64_t)a.dnx * DS;
     const int first = a.dnx == a.L ? 0 : a.rank * a.l;
-    for (int idx = threadIdx.x; idx < a.dnx * DS; idx += BT) {
+    const int e0 = z * RAE_IDX_EPS, e1 = min(e0 + RAE_IDX_EPS, a.dnx);
+    for (int idx = e0 * DS + threadIdx.x; idx < e1 * DS; idx += BT) {
         const int bl = idx / DS, t = idx - bl * DS;
         const int bg = first + bl;
         const int64_t ex = g * (int64_t)a.L + bg;

@@ -135,11 +135,14 @@ struct StepArgs {
     // row index of the global batches (rae_index.hpp), one slot per batch % index_window
     int HA, HW, RA, RW, posbits;
     int64_t index_window;
-    int32_t *hdrA, *srecA, *urowA;      // urow*: interleaved (row, first position) pairs
-    int32_t *hdrW, *srecW, *urowW;
-    int32_t *srowA, *srowW;             // build scratch: the rows of the records binned by partition
-    int32_t *vrowA, *vrowW;             // very heavy rows' segments (VCA / VCW per slot)
-    int VCA, VCW;
+    int32_t *srecA, *urowA;             // sorted record ids; urow*: the partitions' segments
+    int32_t *srecW, *urowW;             // (row, first position, end, first record), class-ordered
+    unsigned long long *skeyA, *skeyW;  // build scratch: (row, record) keys binned by partition
+    int32_t* gidx;                      // build scratch: per slot and table, partition counts +
+                                        // scatter cursors (RAE_IDX_HMAX each; zeroed per build)
+    int32_t* pcls;                      // per slot, table, partition: (heavy, light, very heavy,
+                                        // offset) -- k_build_tasks' input
+    int VCA, VCW;                       // bounds on the very heavy rows of a batch
     // the update's dispatch table per slot (rae_index.hpp build_batch_tasks): every row task in
     // dispatch order (W rows as ~row), the first NVC very heavy rows as workgroup tasks, and a
     // header (tasks, workgroup tasks) -- one load away from the wave that runs the task
