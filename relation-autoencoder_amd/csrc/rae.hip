@@ -179,16 +179,18 @@ __global__ __launch_bounds__(RAE_BT) void k_idx_scatter(StepArgs a, int64_t firs
     const int64_t g = first + blockIdx.x;
     index_scatter<RAE_BT>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, sh);
 }
+template <bool BIG>
 __global__ __launch_bounds__(RAE_FBT) void k_idx_sort(StepArgs a, int64_t first) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = first + blockIdx.x;
-    index_sort<RAE_FBT>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, smem);
+    index_sort<RAE_FBT, BIG>(a, g, g % a.index_window, blockIdx.y, blockIdx.z, smem);
 }
-// the update's dispatch tables of the same batches (after k_idx_sort)
+// the update's dispatch tables of the same batches (after k_idx_sort): blockIdx.y = range of
+// RAE_TASK_PER table entries
 __global__ __launch_bounds__(RAE_BT) void k_build_tasks(StepArgs a, int64_t first) {
     __shared__ int sh[6 * (RAE_IDX_HMAX + 1)];
     const int64_t g = first + blockIdx.x;
-    build_batch_tasks<RAE_BT>(a, g, g % a.index_window, sh);
+    build_batch_tasks<RAE_BT>(a, g, g % a.index_window, blockIdx.y, sh);
 }
 
 // partitioned data-parallel update (rae_dp.hpp): the peers' row lists of global batches
@@ -603,7 +605,8 @@ struct rae_plan {
     int* h_err = nullptr;   // pinned host word of rae_check_on
     char* ws = nullptr;
     size_t smem_fwd = 0;
-    size_t smem_idx = 0;
+    size_t smem_idx = 0;    // k_idx_sort<true> (partitions of more than RAE_IDX_FAST keys)
+    size_t smem_idxf = 0;   // k_idx_sort<false>
     size_t smem_dec = 0;
     size_t smem_mt = 0;     // k_bil_mt: one 8 x 16 x m block of R in LDS
     size_t smem_mt0 = 0;    // ... its first pass (no transposed image for dP): less LDS per WG
@@ -990,8 +993,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
 
     const int ex_floats = example_smem_floats(c.decoder, c.relations, c.embed, c.neg_samples);
     const size_t smem_ex = 4ull * ex_floats;
-    // k_idx_sort: keys, scan scratch, segment starts
-    p->smem_idx = 8ull * RAE_KCAP + 4ull * 32 + 4ull * RAE_KCAP;
+    // k_idx_sort<big>: keys, scan scratch, segment starts (the fast form: RAE_IDX_FAST keys)
+    p->smem_idx = 8ull * RAE_KCAP + 4ull * 64 + 4ull * RAE_KCAP;
+    p->smem_idxf = 8ull * RAE_IDX_FAST + 4ull * 64 + 4ull * RAE_IDX_FAST;
     p->smem_fwd = smem_ex;
     p->smem_spe = p->sp_split ? 4ull * example_smem_floats(0, c.relations, c.embed, 0) : 0;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
@@ -1055,7 +1059,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
             (void)hipFuncSetAttribute((const void*)k_bil_dec<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_dec);
         }
-        (void)hipFuncSetAttribute((const void*)k_idx_sort,
+        (void)hipFuncSetAttribute((const void*)k_idx_sort<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->smem_idx);
         (void)hipFuncSetAttribute((const void*)k_build_dplists,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1317,10 +1321,14 @@ static int launch_index(rae_plan* p, int64_t first, int64_t count, hipStream_t s
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_idx_scatter, dim3((unsigned)count, 2, nsl), dim3(RAE_BT), 0, st, a, first);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_idx_sort, dim3((unsigned)count, 2, hmax), dim3(RAE_FBT), p->smem_idx, st,
-                       a, first);
+    hipLaunchKernelGGL(k_idx_sort<false>, dim3((unsigned)count, 2, hmax), dim3(RAE_FBT),
+                       p->smem_idxf, st, a, first);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count), dim3(RAE_BT), 0, st, a, first);
+    hipLaunchKernelGGL(k_idx_sort<true>, dim3((unsigned)count, 2, hmax), dim3(RAE_FBT),
+                       p->smem_idx, st, a, first);
+    HIPCHK(hipGetLastError());
+    const unsigned ntk = (unsigned)((a.TC + RAE_TASK_PER - 1) / RAE_TASK_PER);
+    hipLaunchKernelGGL(k_build_tasks, dim3((unsigned)count, ntk), dim3(RAE_BT), 0, st, a, first);
     HIPCHK(hipGetLastError());
     if (p->args.part) {
         hipLaunchKernelGGL(k_build_dplists, dim3((unsigned)count, p->args.G, 4), dim3(RAE_FBT),

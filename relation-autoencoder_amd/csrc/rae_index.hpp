@@ -291,22 +291,114 @@ __device__ void index_scatter(const StepArgs& a, int64_t g, int64_t slot, int ta
     });
 }
 
-// k_idx_sort: partition h of a table
+// exclusive block-wide prefix sums of NF flags per thread at once: one ballot per flag and wave,
+// one barrier pair for all of them (ws >= NF * BT / 64 ints)
+template <int BT, int NF>
+__device__ __forceinline__ void block_flags_scan(const bool (&f)[NF], int* ws, int (&pre)[NF],
+                                                 int (&tot)[NF]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int in[NF];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+        const unsigned long long bal = __ballot(f[q]);
+        in[q] = __popcll(bal & lt);
+        if (lane == 0) ws[q * (BT / 64) + w] = __popcll(bal);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+        int off = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < BT / 64; ++i) {
+            const int c = ws[q * (BT / 64) + i];
+            off += (i < w) ? c : 0;
+            t += c;
+        }
+        pre[q] = off + in[q];
+        tot[q] = t;
+    }
+}
+
+// Bitonic sort of the partition's keys held in registers, RAE_IDX_KPT per thread (position
+// p = KPT tid + e), over the first n2 (a power of two <= KPT BT) positions: compare-exchange
+// partners inside a thread are register pairs, inside a wave DPP / permlane lane swaps, across
+// waves an LDS round (keys, KPT BT entries) -- 6 of the 66 steps at 2048 keys carry a barrier,
+// where the all-LDS sort had a barrier and four LDS accesses per step.
+#define RAE_IDX_KPT 4
+#define RAE_IDX_FAST (RAE_IDX_KPT * RAE_FBT)    // partitions of up to 2048 keys: k_idx_sort
+// one compare-exchange step (k = 2^LK, j = 2^LJ) on the register keys
+template <int BT, int LK, int LJ>
+__device__ __forceinline__ void reg_bitonic_step(unsigned long long (&kv)[RAE_IDX_KPT],
+                                                 unsigned long long* keys) {
+    constexpr int KPT = RAE_IDX_KPT, k = 1 << LK, j = 1 << LJ;
+    const int tid = threadIdx.x;
+    unsigned long long pv[KPT];
+    if constexpr (j >= KPT * RAE_WAVE) {              // partner in another wave: LDS
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) keys[KPT * tid + e] = kv[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) pv[e] = keys[(KPT * tid + e) ^ j];
+        __syncthreads();
+    } else if constexpr (j >= KPT) {                  // partner lane: lane ^ (j / KPT)
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) pv[e] = xor_lane_u64(kv[e], j / KPT);
+    } else {                                          // partner register
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) pv[e] = kv[e ^ j];
+    }
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) {
+        const int p = KPT * tid + e;
+        const bool take_min = ((p & k) == 0) == ((p & j) == 0);
+        const unsigned long long lo = kv[e] < pv[e] ? kv[e] : pv[e];
+        const unsigned long long hi = kv[e] < pv[e] ? pv[e] : kv[e];
+        kv[e] = take_min ? lo : hi;
+    }
+}
+template <int BT, int LK, int LJ>
+__device__ __forceinline__ void reg_bitonic_level(unsigned long long (&kv)[RAE_IDX_KPT],
+                                                  unsigned long long* keys) {
+    reg_bitonic_step<BT, LK, LJ>(kv, keys);
+    if constexpr (LJ > 0) reg_bitonic_level<BT, LK, LJ - 1>(kv, keys);
+}
+template <int BT, int LK, int LOGN>
+__device__ __forceinline__ void reg_bitonic_levels(unsigned long long (&kv)[RAE_IDX_KPT], int n2,
+                                                   unsigned long long* keys) {
+    if ((1 << LK) > n2) return;                      // uniform: the first n2 positions are sorted
+    reg_bitonic_level<BT, LK, LK - 1>(kv, keys);
+    if constexpr (LK < LOGN) reg_bitonic_levels<BT, LK + 1, LOGN>(kv, n2, keys);
+}
 template <int BT>
+__device__ __forceinline__ void reg_bitonic_sort(unsigned long long (&kv)[RAE_IDX_KPT], int n2,
+                                                 unsigned long long* keys) {
+    constexpr int LOGN = 11;                          // 2^11 = KPT * BT (BT = 512)
+    static_assert(RAE_IDX_KPT * BT == (1 << LOGN), "fast sort size");
+    reg_bitonic_levels<BT, 1, LOGN>(kv, n2, keys);
+}
+
+// k_idx_sort (big = false: partitions of up to RAE_IDX_FAST keys, register sort, small LDS ->
+// several workgroups per CU) and k_idx_sort_big (the rare larger partitions, up to RAE_KCAP
+// keys, LDS sort): partition h of a table
+template <int BT, bool BIG>
 __device__ void index_sort(const StepArgs& a, int64_t g, int64_t slot, int tab, int h, char* smem) {
     const int tid = threadIdx.x;
     const IdxTab t = idx_tab(a, g, slot, tab);
     if (h >= t.H || t.H > RAE_IDX_HMAX || t.nrec > t.Rcap) return;
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-    int* sint = reinterpret_cast<int*>(keys + RAE_KCAP);    // [0..31] scan scratch
-    int* sstart = sint + 32;                                 // segment starts (<= RAE_KCAP)
     const int32_t* gc = idx_gc(a, slot, tab, 0);
+    const int cnt = gc[h];
+    if (BIG != (cnt > RAE_IDX_FAST)) return;            // the other launch's partition
+    constexpr int KC = BIG ? RAE_KCAP : RAE_IDX_FAST;
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+    int* sint = reinterpret_cast<int*>(keys + KC);      // [0..63] scan scratch
+    int* sstart = sint + 64;                             // segment starts (<= KC)
     // the partition's offset: the counts of partitions 0..h-1
     int part = 0;
     for (int k = tid; k < h; k += BT) part += gc[k];
     int base;
     block_int_scan<BT>(part, sint, &base);
-    const int cnt = gc[h];
     int4* cls = idx_cls(a, slot, tab);
     if (cnt > RAE_KCAP) {
         if (tid == 0) {
@@ -315,26 +407,39 @@ __device__ void index_sort(const StepArgs& a, int64_t g, int64_t slot, int tab, 
         }
         return;
     }
-    for (int i = tid; i < cnt; i += BT) keys[i] = t.skey[base + i];
     int n2 = 1;
     while (n2 < cnt) n2 <<= 1;
-    for (int i = cnt + tid; i < n2; i += BT) keys[i] = ~0ull;
-    __syncthreads();
-    lds_bitonic_sort<BT>(keys, n2);
+    if constexpr (BIG) {
+        for (int i = tid; i < cnt; i += BT) keys[i] = t.skey[base + i];
+        for (int i = cnt + tid; i < n2; i += BT) keys[i] = ~0ull;
+        __syncthreads();
+        lds_bitonic_sort<BT>(keys, n2);
+    } else {
+        unsigned long long kv[RAE_IDX_KPT];
+#pragma unroll
+        for (int e = 0; e < RAE_IDX_KPT; ++e) {
+            const int p = RAE_IDX_KPT * tid + e;
+            kv[e] = p < cnt ? t.skey[base + p] : ~0ull;
+        }
+        reg_bitonic_sort<BT>(kv, n2, keys);
+#pragma unroll
+        for (int e = 0; e < RAE_IDX_KPT; ++e) keys[RAE_IDX_KPT * tid + e] = kv[e];
+        __syncthreads();
+    }
     // segment heads in sorted order -> sstart[segment]
     int nu = 0;
     for (int i0 = 0; i0 < cnt; i0 += BT) {
         const int i = i0 + tid;
-        int head = 0;
+        bool head[1] = {false};
         if (i < cnt) {
             const unsigned long long k = keys[i];
-            head = (i == 0) || ((unsigned)(keys[i - 1] >> 32) != (unsigned)(k >> 32));
+            head[0] = (i == 0) || ((unsigned)(keys[i - 1] >> 32) != (unsigned)(k >> 32));
             t.srec[base + i] = (int32_t)(unsigned)(k & 0xffffffffull);
         }
-        int tot;
-        const int u = nu + block_flag_scan<BT>(head, sint + 1, &tot);
-        if (head) sstart[u] = i;
-        nu += tot;
+        int pre[1], tot[1];
+        block_flags_scan<BT, 1>(head, sint, pre, tot);
+        if (head[0]) sstart[nu + pre[0]] = i;
+        nu += tot[0];
     }
     __syncthreads();
     const int64_t ex0 = g * (int64_t)a.L;
@@ -375,31 +480,28 @@ __device__ void index_sort(const StepArgs& a, int64_t g, int64_t slot, int tab, 
         const int v = v0 + tid;
         int st, en, c = -1;
         if (v < nu) c = seg_class(v, st, en, false);
+        const bool f[3] = {c == 0, c == 1, c == 2};
+        int pre[3], tot[3];
+        block_flags_scan<BT, 3>(f, sint, pre, tot);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            int tot;
-            block_flag_scan<BT>(c == k, sint + 1, &tot);
-            n[k] += tot;
-        }
+        for (int k = 0; k < 3; ++k) n[k] += tot[k];
     }
     int o[3] = {0, n[0], n[0] + n[1]};
     for (int v0 = 0; v0 < nu; v0 += BT) {
         const int v = v0 + tid;
         int st = 0, en = 0, c = -1;
         if (v < nu) c = seg_class(v, st, en, true);
-        int pos = 0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            int tot;
-            const int p = block_flag_scan<BT>(c == k, sint + 1, &tot);
-            if (c == k) pos = o[k] + p;
-            o[k] += tot;
-        }
+        const bool f[3] = {c == 0, c == 1, c == 2};
+        int pre[3], tot[3];
+        block_flags_scan<BT, 3>(f, sint, pre, tot);
         if (c >= 0 && c < 3) {
             const unsigned long long k = keys[st];
+            const int pos = c == 0 ? o[0] + pre[0] : (c == 1 ? o[1] + pre[1] : o[2] + pre[2]);
             t.seg[base + pos] = make_int4((int)(unsigned)(k >> 32), base + st, base + en,
-                                          (int)(unsigned)(k & 0xffffffffull));
+                                                    (int)(unsigned)(k & 0xffffffffull));
         }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[k] += tot[k];
     }
     if (tid == 0) cls[h] = make_int4(n[0], n[1], n[2], base);
 }
@@ -408,15 +510,17 @@ __device__ void index_sort(const StepArgs& a, int64_t g, int64_t slot, int tab, 
 // the update's row waves then find their task with ONE load issued at wave start in parallel
 // with the table header.
 //   vtask[slot][v]  very heavy rows (A first, then W), v < NVC: one workgroup each
-//   task[slot][t]   wave tasks in dispatch order: very heavy rows beyond NVC, heavy A, heavy W,
-//                   light A, light W
+//   task[slot][t]   wave tasks in dispatch order: heavy A, heavy W, light A, light W, then the
+//                   very heavy rows beyond NVC (none at all in plans whose NVC covers them)
 //   thdr[slot]      (wave tasks, workgroup tasks, chunked rows, 0)
-// W rows are stored as ~row (negative), A rows as row.
+// W rows are stored as ~row (negative), A rows as row.  Workgroup z of the batch copies table
+// entries [z RAE_TASK_PER, (z + 1) RAE_TASK_PER); workgroup 0 also lays out the very heavy rows.
 // LDS: for each table and class (heavy, light, very heavy) the exclusive prefix of the
 // partitions' class counts (RAE_IDX_HMAX + 1 ints each); an entry's partition is found by
 // binary search there.
+#define RAE_TASK_PER 2048
 template <int BT>
-__device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, int* sh) {
+__device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, int z, int* sh) {
     __shared__ int sws[BT / 64];
     int Ht[2];
     const int4* clsT[2] = {idx_cls(a, slot, 0), idx_cls(a, slot, 1)};
@@ -426,17 +530,15 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, in
         if (Ht[tab] > RAE_IDX_HMAX) Ht[tab] = 0;           // flagged by k_idx_count
         for (int c = 0; c < 3; ++c) {
             int* pf = sh + (tab * 3 + c) * (RAE_IDX_HMAX + 1);
+            int x = 0;
             for (int h = threadIdx.x; h < Ht[tab]; h += BT) {
                 const int4 q = clsT[tab][h];
                 pf[h] = c == 0 ? q.x : (c == 1 ? q.y : q.z);
+                x += pf[h];
             }
-            __syncthreads();
-            int x = 0;
-            for (int h = threadIdx.x; h < Ht[tab]; h += BT) x += pf[h];
             int t_;
             block_int_scan<BT>(x, sws, &t_);
             tot[tab][c] = t_;
-            if (threadIdx.x == 0) pf[Ht[tab]] = t_;
             lds_exclusive_scan<BT>(pf, Ht[tab], sws);
         }
     }
@@ -457,8 +559,19 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, in
     };
     const int VA = tot[0][2], VW = tot[1][2];
     const int HA = tot[0][0], HW = tot[1][0], LA = tot[0][1], LW = tot[1][1];
+    const int TH = HA + HW + LA + LW;
     int4* vt = reinterpret_cast<int4*>(a.vtask) + slot * a.NVC;
     int4* tk = reinterpret_cast<int4*>(a.task) + slot * a.TC;
+    for (int t = z * RAE_TASK_PER + threadIdx.x; t < min(TH, (z + 1) * RAE_TASK_PER); t += BT) {
+        int x = t;
+        int4 sg;
+        if (x < HA) sg = seg_of(0, 0, x);
+        else if ((x -= HA) < HW) sg = seg_of(1, 0, x);
+        else if ((x -= HW) < LA) sg = seg_of(0, 1, x);
+        else sg = seg_of(1, 1, x - LA);
+        tk[t] = sg;
+    }
+    if (z != 0) return;
     auto vrow = [&](int v) { return v < VA ? seg_of(0, 2, v) : seg_of(1, 2, v - VA); };
     // very heavy rows: rows with at least 2 hch records become floor(records / hch) chunk tasks
     // (the first vtask entries; chunk k = records [st + k hch, st + (k+1) hch), the last one
@@ -504,22 +617,12 @@ __device__ void build_batch_tasks(const StepArgs& a, int64_t g, int64_t slot, in
         const int i = NC + NU + block_int_scan<BT>(un ? 1 : 0, sws, &tu);
         if (un) {
             if (i < a.NVC) vt[i] = sg;
-            else tk[i - a.NVC] = sg;
+            else tk[TH + i - a.NVC] = sg;
         }
         NU += tu;
     }
     const int NV = min(NC + NU, a.NVC), XV = NC + NU - NV;
-    const int T = XV + HA + HW + LA + LW;
-    for (int t = threadIdx.x; t < T - XV; t += BT) {
-        int x = t;
-        int4 sg;
-        if (x < HA) sg = seg_of(0, 0, x);
-        else if ((x -= HA) < HW) sg = seg_of(1, 0, x);
-        else if ((x -= HW) < LA) sg = seg_of(0, 1, x);
-        else sg = seg_of(1, 1, x - LA);
-        tk[XV + t] = sg;
-    }
-    if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(T, NV, NF, 0);
+    if (threadIdx.x == 0) reinterpret_cast<int4*>(a.thdr)[slot] = make_int4(TH + XV, NV, NF, 0);
 }
 
 // Per-example descriptors of the rank's l examples of batch g (slot): everything the forward
