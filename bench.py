@@ -8,11 +8,11 @@ decoder forward/backward + AdaGrad update of every parameter.  Inputs (dataset, 
 negatives) are resident in HBM before the timed region; negative sampling (host RNG, as in
 the reference) is timed separately.  K steps are timed between barrier+synchronize pairs,
 max over ranks.  The parameter-independent row index is built as the epoch loop builds it
-(engine index_overlap): the next window's index on a side stream beside the steps -- so the
-timed region holds the K steps AND the index build of the next K batches, running
-concurrently; value = K * global_batch / seconds (a build the ring cannot hold beside the
-steps is added at its serial per-batch cost) -- end-to-end training throughput.  Rank 0
-prints one JSON line.
+(engine index_overlap): for K >= OVERLAP_MIN_STEPS the next window's index on a side stream
+beside the steps -- the timed region holds the K steps AND the index build of the next K
+batches, running concurrently; shorter runs (the driver's 20 steps) time the steps alone and
+add the index at its serial per-batch cost measured over a whole window; value =
+K * global_batch / seconds -- end-to-end training throughput.  Rank 0 prints one JSON line.
 
 Also reported: the roofline of the step's dominant kernel (the one with the longest average
 launch; algorithmic bytes per launch by SURVEY.md 8(d)'s accounting / its average duration
@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "relation-autoencoder_amd"))
 
 METRIC = "train examples/sec (fwd+bwd) K=100 d=200 neg=20 at 1/2/4/8 MI355X"
+OVERLAP_MIN_STEPS = 128     # timed runs this long build the next batches' index beside the steps
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (v_mfma_f32_16x16x4_f32)
 MFMA_BF16_PEAK_TFS = 2500.0
@@ -325,9 +326,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     # the index of the K batches after the timed ones, built beside them as the epoch loop
-    # builds a window's successor (engine.run prefetch)
+    # builds a window's successor (engine.run prefetch) -- for runs of at least
+    # OVERLAP_MIN_STEPS steps; a shorter run is timed without it and the build is counted at its
+    # serial per-batch cost over a whole window (measured below): beside only 20 steps the side
+    # build's interference costs the steps more (0.6-0.8 us each, profiles/r05_ab.txt) than the
+    # whole serial build (0.39 us per batch)
     npref = 0
-    if prebuilt and eng.index_overlap and 2 * K <= eng.index_window:
+    if prebuilt and eng.index_overlap and 2 * K <= eng.index_window and K >= OVERLAP_MIN_STEPS:
         npref = max(0, min(K, nb - W - K))
     # no run follows the timed one on this cursor: its last graph skips the cursor advance
     eng.run(W, K, index=not prebuilt, last_advance=False,
@@ -609,6 +614,9 @@ def main():
                         "over a whole window)"),
         "index_batches_built_in_timed_region": npref if prebuilt else K,
         "index_overlap": eng.index_overlap,
+        "index_mode": ("beside the timed steps (side stream)" if npref > 0 else
+                       "serial, counted at index_build_us_per_batch per step") if prebuilt else
+                      "on the step stream before each window (inside the timed region)",
         "build_id": build_id,
         "dataset_build_s": t_data,
     }

@@ -40,6 +40,14 @@ for st in "$@"; do
       timeout -k 10 300 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-label-pass > $O/drvq.json 2> $O/drvq.err \
         || { echo drvq bench failed; tail -30 $O/drvq.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/drvq.json')); print('drvq', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), 'hostq', round(d['timed_region_host_queue_us'],1), {k: round(v, 2) for k, v in d['kernel_us'].items()})" ;;
+    rep:*)
+      # the driver's command n times (timing only; "rep:3" or "rep:3:--no-index-overlap")
+      a=${st#rep:}; n=${a%%:*}; x=""; [ "$a" != "$n" ] && x=${a#*:}
+      for i in $(seq 1 $n); do
+        timeout -k 10 300 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-label-pass $x > $O/rep_$i.json 2> $O/rep_$i.err \
+          || { echo rep bench failed; tail -30 $O/rep_$i.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/rep_$i.json')); print('rep $x', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), 'hostq', round(d['timed_region_host_queue_us'],1), 'idx', round(d['index_build_us_per_batch'], 3), {k: round(v, 2) for k, v in d['kernel_us'].items()})"
+      done ;;
     b512)
       timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-label-pass > $O/b512.json 2> $O/b512.err \
         || { echo b512 bench failed; tail -30 $O/b512.err; exit 1; }
