@@ -261,7 +261,14 @@ def main():
     ap.add_argument("--dp-update", default="replicated", choices=["replicated", "partitioned"],
                     help="data-parallel update (N > 1): every rank updates every row, or each "
                          "rank the rows it owns (rows pulled from their owners each step)")
+    ap.add_argument("--dp-xchg", default="collective", choices=["collective", "p2p"],
+                    help="partitioned update, N > 1: RCCL collectives between the step launches, or "
+                         "the kernels' own stores into the peers' IPC-mapped buffers (include/rae.h "
+                         "RAE_XCHG_P2P)")
     args = ap.parse_args()
+    if args.dp_xchg == "p2p":
+        args.dp_update = "partitioned"
+        args.kernel_form.append("dp_xchg=p2p")
 
     import torch
     from rae import dist as rdist
@@ -317,7 +324,8 @@ def main():
     if eng._dp:                            # the rows all-to-all's communicator, before capture
         if not prebuilt:
             eng.build_index(0, min(eng.index_window, W + K))
-        exchange.rows(eng._dp_send, eng._dp_recv)
+        if not eng._p2p:
+            exchange.rows(eng._dp_send, eng._dp_recv)
         torch.cuda.synchronize()
     graphed = warm_up(eng, W, K, prebuilt, args.graph_chunk > 1)
     timed_graphs = eng.graph_sizes(W, K) if graphed else []
@@ -377,7 +385,7 @@ def main():
     xev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(n_it)]
     pev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(n_it)]
     for i in range(n_it):
-        if eng._dp:                        # partitioned update: rows pulled from their owners
+        if eng._dp and not eng._p2p:       # partitioned update: rows pulled from their owners
             pev[i][0].record(st)
             assert lib.rae_dp_pack(plan, i, sp_) == 0, lib.rae_last_error()
             exchange.rows(eng._dp_send, eng._dp_recv)
@@ -385,7 +393,7 @@ def main():
             pev[i][1].record(st)
         assert lib.rae_time_next(plan, fev[i][0], fev[i][1]) == 0
         assert lib.rae_step_forward(plan, i, sp_) == 0, lib.rae_last_error()
-        if exchange is not None:           # the all-gather of the records (data-parallel only)
+        if exchange is not None and not eng._p2p:   # the records all-gather (data parallel)
             xev[i][0].record(st)
             exchange(eng.exchange_buf)
             xev[i][1].record(st)
@@ -399,7 +407,8 @@ def main():
         return v.value
     fwd_ms = np.array([_ms(e) for e in fev])
     upd_ms = np.array([_ms(e) for e in uev])
-    xch_ms = np.array([a.elapsed_time(b) for a, b in xev]) if exchange is not None else None
+    xch_ms = np.array([a.elapsed_time(b) for a, b in xev]) \
+        if exchange is not None and not eng._p2p else None
     for e in fev + uev:
         lib.rae_event_destroy(e[0])
         lib.rae_event_destroy(e[1])
@@ -622,7 +631,7 @@ def main():
     }
     if xch_ms is not None:
         out["kernel_us"]["exchange"] = float(np.mean(xch_ms) * 1e3)
-    if eng._dp:
+    if eng._dp and not eng._p2p:
         out["kernel_us"]["row_pull"] = float(np.mean([a.elapsed_time(b) for a, b in pev]) * 1e3)
         out["config"]["dp_row_caps"] = list(eng._dp_caps)
     if rk == 0 and ws == 1 and not args.no_cpu_baseline:

@@ -43,6 +43,9 @@ typedef struct ihipStream_t* rae_stream_t;   /* == hipStream_t */
 #define RAE_E_HIP (-2)         /* HIP runtime error                                  */
 #define RAE_E_OVERFLOW (-3)    /* a per-step row-index partition overflowed its LDS  */
 #define RAE_E_STATE (-4)       /* call sequence error                                */
+/* device error word bits (rae_check): 1 / 2 an A / W row-index partition overflowed its LDS
+ * sort, 4 a batch exceeded the index's record capacity, 8 / 16 a data-parallel row list
+ * overflowed, 64 a peer-to-peer wait timed out (a peer stopped signalling)                 */
 
 /* decoder type: learning/models/decoders/Decoder.py:84-93 ('sp', 'rescal', 'rescal+sp') */
 #define RAE_DEC_SP 0
@@ -90,6 +93,7 @@ typedef struct rae_config {
     int32_t priv_rows;        /* rows one record of the batch references: RAE_PRIV_*        */
     int32_t dp_dense;         /* data-parallel SP: dense decoder-matrix gradients RAE_DPDENSE_* */
     int32_t heavy_chunk;      /* very heavy rows split into record chunks: RAE_HCHUNK_*      */
+    int32_t dp_xchg;          /* data-parallel exchange: RAE_XCHG_*                          */
 } rae_config;
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
@@ -130,6 +134,11 @@ typedef struct rae_config {
                                * applies the optimiser); smaller batches: off                    */
 #define RAE_HCHUNK_OFF 1      /* every very heavy row summed by one workgroup                      */
 #define RAE_HCHUNK_ON 2       /* chunks at any global batch                                        */
+#define RAE_XCHG_COLLECTIVE 0 /* the caller moves records / rows between the step launches (an    *
+                               * all-gather; rae_dp_pack -> all-to-all -> rae_dp_unpack)         */
+#define RAE_XCHG_P2P 1        /* partitioned update only: the kernels store records and rows     *
+                               * straight into the peers' buffers (rae_set_peer) and wait on     *
+                               * their signal counters -- no caller collective in the step       */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]
@@ -238,6 +247,26 @@ int rae_dp_pack(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
 int rae_dp_unpack(rae_plan* plan, int64_t step_offset, rae_stream_t stream);
 int rae_dp_pack_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
 int rae_dp_unpack_at(rae_plan* plan, int64_t batch, rae_stream_t stream);
+
+/* --- peer-to-peer exchange (dp_xchg = RAE_XCHG_P2P) ---------------------------------- *
+ * Every rank maps its peers' exchange buffer, W, A, Ab and signal words (IPC handles, traded
+ * once through the caller's process group) and hands them to its plan; rae_step_forward then
+ * pushes the owned rows each peer's examples read into that peer's replica, waits for the
+ * peers' rows, runs the forward and pushes its records into every peer's exchange buffer;
+ * rae_step_update waits for the peers' records.  Graph-capturable (kernels only).  The row
+ * capacities come from rae_set_dp_buffers(plan, NULL, NULL, caps) as in the collective form.
+ * Replaces (learning/OieInduction.py:186-189 runs one process): the all-gather / all-to-all. */
+#define RAE_IPC_HANDLE_BYTES 64
+/* handle of the allocation holding dev_ptr, and dev_ptr's offset in it                     */
+int rae_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out);
+/* map another process's allocation (its base address; add the exported offset)            */
+int rae_ipc_open(const void* handle, void** base_out);
+int rae_ipc_close(void* base);
+/* the plan's signal counters (device; export them to the peers)                            */
+void* rae_p2p_signals(rae_plan* plan);
+/* peer `peer`'s buffers as this process maps them                                          */
+int rae_set_peer(rae_plan* plan, int32_t peer, float* exchange_dev, float* W_dev, float* A_dev,
+                 float* Ab_dev, void* signals_dev);
 
 /* Kernel timing (bench / profiling; no reference counterpart).  Arms the NEXT
  * rae_step_forward or rae_step_update call on this plan: its kernels are launched with

@@ -29,6 +29,7 @@
 #include "rae_dp.hpp"
 #include "rae_index.hpp"
 #include "rae_label.hpp"
+#include "rae_p2p.hpp"
 #include "rae_sampler.hpp"
 #include "rae_sp.hpp"
 #include "rae_step.hpp"
@@ -37,6 +38,9 @@
 using namespace rae;
 
 #define RAE_VERSION 1
+#ifndef RAE_P2P_GRID
+#define RAE_P2P_GRID 256      // workgroups of a peer-to-peer push (each signals every peer)
+#endif
 #ifndef RAE_UPD_WPE
 #define RAE_UPD_WPE 5   // SP update: <= 102 VGPRs -> 20 waves per CU (6: 85 VGPRs spilled the
                         // Q = 2 rows of C4 -- 23.8 vs 20.2 us update; r03_ab.txt)
@@ -200,6 +204,12 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_dplists(StepArgs a, int64_t f
     const int64_t g = first + blockIdx.x;
     build_dp_list<RAE_FBT>(a, g, g % a.index_window, blockIdx.z >> 1, blockIdx.y, blockIdx.z & 1,
                            smem);
+}
+// peer-to-peer exchange (rae_p2p.hpp)
+__global__ __launch_bounds__(RAE_BT) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
+__global__ __launch_bounds__(RAE_BT) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
+__global__ __launch_bounds__(64) void k_p2p_wait(StepArgs a, int kind, unsigned per) {
+    p2p_wait(a, kind, per);
 }
 template <bool PACK>
 __global__ __launch_bounds__(RAE_BT) void k_dp_move(StepArgs a) {
@@ -603,6 +613,9 @@ struct rae_plan {
     int64_t* d_zero = nullptr;
     int* d_err = nullptr;
     int* h_err = nullptr;   // pinned host word of rae_check_on
+    unsigned* d_sig = nullptr;  // peer-to-peer signal counters (own allocation: IPC-exported)
+    bool peers_set = false;     // rae_set_peer called for every other rank
+    int peers_mask = 0;
     char* ws = nullptr;
     size_t smem_fwd = 0;
     size_t smem_idx = 0;    // k_idx_sort<true> (partitions of more than RAE_IDX_FAST keys)
@@ -693,9 +706,13 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.dp_update < RAE_DPUPD_REPLICATED || c.dp_update > RAE_DPUPD_PARTITIONED ||
         c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_ON ||
         c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS ||
-        c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON)
+        c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON ||
+        c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
-                                   "priv_rows / dp_dense / heavy_chunk)");
+                                   "priv_rows / dp_dense / heavy_chunk / dp_xchg)");
+    if (c.dp_xchg == RAE_XCHG_P2P && (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31))
+        return fail(RAE_E_INVALID, "the peer-to-peer exchange runs the partitioned update "
+                                   "(world_size <= 31)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -903,6 +920,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_dpl = a.part ? take(4ull * W_ * dpl_slot_ints(a.G, a.LA, a.LW)) : 0;
     const size_t o_dpc = a.part ? take(4ull * W_ * 2 * a.G * 2) : 0;
     const size_t o_dpm = take(16);
+    // peer-to-peer exchange: the peers' mapped buffers and this rank's expected signal counts
+    const size_t o_peers = take(sizeof(PeerBufs) * (size_t)c.world_size);
+    const size_t o_pexp = take(4ull * 2 * c.world_size);
     const bool bil = c.decoder != RAE_DEC_SP;
     a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
     // bf16 dP with LDS-staged R slices (k_bil_dp2): the C5 shape compiled exactly, other
@@ -954,6 +974,16 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     }
     *p->h_err = 0;
+    if (c.dp_xchg == RAE_XCHG_P2P) {
+        e = hipMalloc(reinterpret_cast<void**>(&p->d_sig), 4ull * 2 * c.world_size);
+        if (e == hipSuccess) e = hipMemset(p->d_sig, 0, 4ull * 2 * c.world_size);
+        if (e != hipSuccess) {
+            (void)hipFree(p->ws);
+            (void)hipHostFree(p->h_err);
+            delete p;
+            return fail(RAE_E_HIP, std::string("hipMalloc signals: ") + hipGetErrorString(e));
+        }
+    }
     p->d_cursor = reinterpret_cast<int64_t*>(p->ws + o_cursor);
     p->d_zero = reinterpret_cast<int64_t*>(p->ws + o_zero);
     p->d_err = reinterpret_cast<int*>(p->ws + o_err);
@@ -987,6 +1017,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.dpl = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpl) : nullptr;
     a.dpc = a.part ? reinterpret_cast<int32_t*>(p->ws + o_dpc) : nullptr;
     a.dpmax = reinterpret_cast<int*>(p->ws + o_dpm);
+    a.xchg = c.dp_xchg;
+    a.peers = reinterpret_cast<PeerBufs*>(p->ws + o_peers);
+    a.p2p_expect = reinterpret_cast<unsigned*>(p->ws + o_pexp);
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
     if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
     if (a.dpart) a.dwb = reinterpret_cast<float*>(p->ws + o_dwb);
@@ -1065,6 +1098,14 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(4 * RAE_DPL_KEYS + 4 * 32));
     }
+    a.sig = p->d_sig;
+    if (a.sig) {                 // this rank's own entry of the peer table
+        const PeerBufs own{a.ex, a.W, a.A, a.Ab, a.sig};
+        if (hipMemcpy(a.peers + c.rank, &own, sizeof(own), hipMemcpyHostToDevice) != hipSuccess) {
+            rae_plan_destroy(p);
+            return fail(RAE_E_HIP, "peer table");
+        }
+    }
     *out = p;
     return RAE_OK;
 }
@@ -1082,6 +1123,7 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
     out->dp_dense = p->args.lay.wire == 2 ? RAE_DPDENSE_PARTIALS
                   : (p->args.lay.wire == 1 ? RAE_DPDENSE_RECORDS : 0);
     out->heavy_chunk = p->args.hch ? RAE_HCHUNK_ON : RAE_HCHUNK_OFF;
+    out->dp_xchg = p->cfg.dp_xchg;
     return RAE_OK;
 }
 
@@ -1089,6 +1131,7 @@ extern "C" int rae_plan_destroy(rae_plan* p) {
     if (!p) return RAE_OK;
     if (p->ws) (void)hipFree(p->ws);
     if (p->h_err) (void)hipHostFree(p->h_err);
+    if (p->d_sig) (void)hipFree(p->d_sig);
     delete p;
     return RAE_OK;
 }
@@ -1182,12 +1225,32 @@ static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         RAE_LAUNCH(p, k_bil_dp<false>, dim3(gd), dim3(RAE_BT), 0, st, a);
 }
 
+// peer-to-peer exchange grids (every rank the same: the peers expect these many signals)
+static unsigned p2p_rows_grid(const StepArgs& a) {
+    const int64_t waves = (int64_t)a.G * (a.capA + a.capW);
+    const int64_t g = (waves + RAE_NWAVE - 1) / RAE_NWAVE;
+    return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
+}
+static unsigned p2p_recs_grid(const StepArgs& a) {
+    const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;
+    const int64_t g = (n4 + RAE_BT - 1) / RAE_BT;
+    return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
+}
+static bool p2p_on(const rae_plan* p) { return p->args.xchg == RAE_XCHG_P2P && p->args.G > 1; }
+
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
     if (!p->args.neg1 || !p->args.neg2) return fail(RAE_E_STATE, "negatives not set");
     StepArgs a = p->args;
     a.cursor = cursor;
     a.step_offset = off;
     a.stamps = p->stamps_fwd;
+    const bool p2p = p2p_on(p);
+    if (p2p) {                // the owned rows the peers' examples read, into their replicas
+        if (!p->peers_set) return fail(RAE_E_STATE, "peer buffers not set (rae_set_peer)");
+        const unsigned gr = p2p_rows_grid(a);
+        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, gr);
+    }
     if (a.dec == RAE_DEC_SP) {
         launch_fwd_sp(p, a, st);
         if (a.dpart)          // this rank's dense partials into its records, before the exchange
@@ -1195,6 +1258,8 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     }
     else if (p->v4) launch_fwd_bil<true>(p, a, st);
     else launch_fwd_bil<false>(p, a, st);
+    if (p2p)                  // this rank's records into every peer's exchange buffer
+        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_BT), 0, st, a);
     p->t_start = p->t_stop = nullptr;
     HIPCHK(hipGetLastError());
     return RAE_OK;
@@ -1255,6 +1320,8 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     a.step_offset = off;
     a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
+    if (p2p_on(p))            // every peer's records of this batch are here
+        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 0, p2p_recs_grid(a));
     if (a.lay.wire)           // the vectors the wire records left out, for the whole batch
     {
         const dim3 gv(ceil_div(vrec_tasks(a.L, a.r), RAE_NWAVE));
@@ -1380,8 +1447,8 @@ extern "C" int rae_set_dp_buffers(rae_plan* p, float* send, float* recv, int32_t
                                   int32_t cap_features) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     if (!p->args.part) return fail(RAE_E_STATE, "the plan's data-parallel update is not partitioned");
-    if (!send || !recv || cap_entities < 0 || cap_features < 0 || cap_entities > p->args.LA ||
-        cap_features > p->args.LW)
+    if ((p->args.xchg != RAE_XCHG_P2P && (!send || !recv)) || cap_entities < 0 || cap_features < 0 ||
+        cap_entities > p->args.LA || cap_features > p->args.LW)
         return fail(RAE_E_INVALID, "bad row-exchange buffers / capacities");
     StepArgs& a = p->args;
     a.dsend = send;
@@ -1404,7 +1471,9 @@ static int launch_dp_move(rae_plan* p, bool pack, const int64_t* cursor, int64_t
     const StepArgs& a0 = p->args;
     if (!a0.part) return fail(RAE_E_STATE, "the plan's data-parallel update is not partitioned");
     if (a0.G == 1) return RAE_OK;                   // every row is this rank's
-    if (!a0.dsend || !a0.drecv) return fail(RAE_E_STATE, "row-exchange buffers not set");
+    if (!a0.dsend || !a0.drecv) return fail(RAE_E_STATE, "row-exchange buffers not set (the "
+                                                       "peer-to-peer exchange has none: its rows "
+                                                       "move inside rae_step_forward)");
     StepArgs a = a0;
     a.cursor = cursor;
     a.step_offset = off;
@@ -1434,6 +1503,46 @@ extern "C" int rae_dp_unpack_at(rae_plan* p, int64_t batch, rae_stream_t stream)
     if (!p) return fail(RAE_E_INVALID, "null plan");
     if (int rc = check_batch(p, batch)) return rc;
     return launch_dp_move(p, false, nullptr, batch, (hipStream_t)stream);
+}
+
+// ---- peer-to-peer exchange (rae_p2p.hpp) ----
+extern "C" int rae_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out) {
+    if (!ptr || !handle_out || !offset_out) return fail(RAE_E_INVALID, "null argument");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIPCHK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr));
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, (void*)base));
+    static_assert(sizeof(h) == RAE_IPC_HANDLE_BYTES, "IPC handle size");
+    memcpy(handle_out, &h, sizeof(h));
+    *offset_out = (int64_t)((const char*)ptr - (const char*)base);
+    return RAE_OK;
+}
+extern "C" int rae_ipc_open(const void* handle, void** base_out) {
+    if (!handle || !base_out) return fail(RAE_E_INVALID, "null argument");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    HIPCHK(hipIpcOpenMemHandle(base_out, h, hipIpcMemLazyEnablePeerAccess));
+    return RAE_OK;
+}
+extern "C" int rae_ipc_close(void* base) {
+    if (!base) return fail(RAE_E_INVALID, "null argument");
+    HIPCHK(hipIpcCloseMemHandle(base));
+    return RAE_OK;
+}
+extern "C" void* rae_p2p_signals(rae_plan* p) { return p ? (void*)p->d_sig : nullptr; }
+extern "C" int rae_set_peer(rae_plan* p, int32_t peer, float* exchange, float* W, float* A,
+                            float* Ab, void* signals) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (p->args.xchg != RAE_XCHG_P2P) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
+    if (peer < 0 || peer >= p->args.G || peer == p->args.rank)
+        return fail(RAE_E_INVALID, "peer must be another rank");
+    if (!exchange || !W || !A || !Ab || !signals) return fail(RAE_E_INVALID, "null peer buffer");
+    const PeerBufs pb{exchange, W, A, Ab, (unsigned*)signals};
+    HIPCHK(hipMemcpy(p->args.peers + peer, &pb, sizeof(pb), hipMemcpyHostToDevice));
+    p->peers_mask |= 1 << peer;
+    p->peers_set = p->peers_mask == (((1 << p->args.G) - 1) & ~(1 << p->args.rank));
+    return RAE_OK;
 }
 
 extern "C" int rae_time_next(rae_plan* p, void* start, void* stop) {

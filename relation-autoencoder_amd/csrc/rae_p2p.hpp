@@ -1,0 +1,116 @@
+// Peer-to-peer data-parallel exchange (rae_config.dp_xchg = RAE_XCHG_P2P; partitioned update).
+//
+// The reference trains on one process (learning/OieInduction.py:186-189); the data-parallel
+// step shards its global batch over G ranks.  With the collective exchange the
+// partitioned step is   pack -> all-to-all -> unpack -> forward -> all-gather -> update, and
+// each collective is a host-launched RCCL call with its own latency on the step's dependence
+// chain.  Here every rank maps its peers' buffers (IPC handles exchanged once at set-up: their
+// exchange buffer, W, A, Ab and signal words) and the kernels store straight into them:
+//   k_p2p_rows   (start of step b, after the update of b-1): the owner stores every row it owns
+//                that peer p's examples of batch b read into p's OWN replica (the row lists of
+//                rae_dp.hpp, direction 0) -- no send buffer, no all-to-all, no unpack
+//   k_p2p_wait   (rows): until every owner's row stores of batch b are visible
+//   forward(b)   this rank's records into its own exchange buffer, as before
+//   k_p2p_recs   its l records into every peer's exchange buffer, at the same rows
+//   k_p2p_wait   (records): until every peer's records of batch b are here
+//   update(b)    the owned rows, as before
+// Signalling: a pushing workgroup's stores are fenced at system scope, then one system-scope
+// atomic add per peer on the peer's signal word (kind, this rank) -- a counter that grows by the
+// push grid's workgroups every step.  The waiting kernel (one wave: lane p watches peer p) spins
+// on acquire loads until each counter reaches its expected value (kept in this rank's private
+// words, advanced by the wait kernel itself, so graph replays stay in step), with a bounded spin:
+// after RAE_P2P_TIMEOUT it sets error bit 64 and returns (the host sees it at rae_check) rather
+// than hold the GPU.
+// Hazards (all ranks run the same step sequence): a peer's replica rows and exchange rows are
+// overwritten only after that peer has consumed them -- owner k's row stores of batch b follow
+// k's update of b - 1, which needed peer p's records of b - 1, which p pushed after its forward
+// of b - 1 (the rows' last reader); k's record stores of batch b follow k's forward of b, which
+// needed p's rows of b, which p pushed after its update of b - 1 (the records' last reader).
+// Each row is stored by its owner only, with the value the collective form would have unpacked,
+// so the parameters are bit-identical to the collective partitioned (and replicated) update.
+#pragma once
+#include "rae_common.hpp"
+#include "rae_dp.hpp"
+#include "rae_step.hpp"
+
+namespace rae {
+
+#ifndef RAE_P2P_TIMEOUT
+#define RAE_P2P_TIMEOUT 500000000ull   // s_memrealtime ticks (100 MHz): 5 s
+#endif
+
+// after a workgroup's peer stores: fence them at system scope, then count this workgroup into
+// every peer's signal word (kind, rank)
+__device__ __forceinline__ void p2p_signal(const StepArgs& a, int kind) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x < a.G && threadIdx.x != a.rank) {
+        unsigned* s = a.peers[threadIdx.x].sig + kind * a.G + a.rank;
+        __hip_atomic_fetch_add(s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// k_p2p_recs: this rank's l records (float4 slices, grid-strided) into every peer's buffer
+__device__ void p2p_push_records(const StepArgs& a) {
+    const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;                 // rec is a multiple of 4
+    const int64_t o4 = (int64_t)a.rank * a.l * a.lay.rec / 4;
+    const float4* src = reinterpret_cast<const float4*>(a.ex) + o4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = src[i];
+        for (int p = 0; p < a.G; ++p)
+            if (p != a.rank) reinterpret_cast<float4*>(a.peers[p].ex)[o4 + i] = v;
+    }
+    p2p_signal(a, 0);
+}
+
+// k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
+// this rank owns that the peer's examples read): the row into the peer's replica
+__device__ void p2p_push_rows(const StepArgs& a) {
+    const int lane = threadIdx.x & 63;
+    const int per = a.capA + a.capW;
+    const int64_t slot = step_batch(a) % a.index_window;
+    for (int64_t t = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+         t < (int64_t)a.G * per; t += (int64_t)gridDim.x * (blockDim.x / 64)) {
+        const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
+        if (p == a.rank) continue;
+        const int tab = i0 >= a.capA ? 1 : 0;
+        const int i = tab ? i0 - a.capA : i0;
+        const int cap = tab ? a.capW : a.capA;
+        const int n = *dpl_count(a, slot, 0, p, tab);
+        if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
+        if (i >= n || i >= cap) continue;
+        const int row = dpl_list(a, slot, 0, p, tab)[i];
+        const int w = tab ? a.m : a.r;
+        const float* s = (tab ? a.W : a.A) + (int64_t)row * w;
+        float* d = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;
+        if ((w & 3) == 0) {
+            for (int c = lane; c < w / 4; c += RAE_WAVE)
+                reinterpret_cast<float4*>(d)[c] = reinterpret_cast<const float4*>(s)[c];
+        } else {
+            for (int c = lane; c < w; c += RAE_WAVE) d[c] = s[c];
+        }
+        if (!tab && lane == 0) a.peers[p].Ab[row] = a.Ab[row];
+    }
+    p2p_signal(a, 1);
+}
+
+// k_p2p_wait: lane p waits for peer p's `per` workgroups of this step (kind 0 records, 1 rows)
+__device__ void p2p_wait(const StepArgs& a, int kind, unsigned per) {
+    const int p = threadIdx.x;
+    if (p >= a.G || p == a.rank) return;
+    unsigned* ex = a.p2p_expect + kind * a.G + p;
+    const unsigned target = *ex + per;
+    const unsigned* s = a.sig + kind * a.G + p;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > RAE_P2P_TIMEOUT) {
+            atomicOr(a.err, 64);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    *ex = target;
+}
+
+}  // namespace rae

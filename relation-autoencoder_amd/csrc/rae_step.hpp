@@ -97,6 +97,16 @@ __host__ __device__ inline RecLayout make_layout(int dec, int m, int r, int s, i
     return L;
 }
 
+// one data-parallel peer's buffers as this rank maps them (rae_set_peer; the peer-to-peer
+// exchange, rae_p2p.hpp); peer == rank: this rank's own
+struct PeerBufs {
+    float* ex;
+    float* W;
+    float* A;
+    float* Ab;
+    unsigned* sig;        // [2 kinds][G writers] signal counters
+};
+
 struct StepArgs {
     // configuration
     int dec, opt;
@@ -199,6 +209,12 @@ struct StepArgs {
     int capA, capW;      // rows per peer block (set with the buffers; <= LA / LW)
     int64_t dblk;
     int* dpmax;          // longest list built since the last rae_dp_list_max [entity, feature]
+    // peer-to-peer exchange (rae.h RAE_XCHG_P2P, rae_p2p.hpp): the peers' mapped buffers, this
+    // rank's signal counters (written by the peers) and its expected counts (private)
+    int xchg;
+    PeerBufs* peers;
+    unsigned* sig;
+    unsigned* p2p_expect;
     // private rows: rows a single record of the global batch references (rae.h RAE_PRIV_AUTO;
     // single-rank SP plans), updated per example by the update launch's leading workgroups;
     // pmask per slot and example = (entity-slot bits j < 32, j >= 32, feature-position bits,

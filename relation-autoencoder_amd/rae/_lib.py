@@ -76,7 +76,9 @@ EXPORTS = (
     "rae_stream_copy", "rae_mfma_probe", "rae_plan_forms",
     "rae_dp_block_floats", "rae_set_dp_buffers", "rae_dp_list_max", "rae_dp_pack",
     "rae_dp_unpack", "rae_dp_pack_at", "rae_dp_unpack_at",
+    "rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_p2p_signals", "rae_set_peer",
 )
+RAE_IPC_HANDLE_BYTES = 64
 
 
 class RaeConfig(C.Structure):
@@ -91,7 +93,7 @@ class RaeConfig(C.Structure):
         ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
         ("sp_forward", C.c_int32), ("bil_dp", C.c_int32), ("bil_prep", C.c_int32),
         ("dp_update", C.c_int32), ("priv_rows", C.c_int32), ("dp_dense", C.c_int32),
-        ("heavy_chunk", C.c_int32),
+        ("heavy_chunk", C.c_int32), ("dp_xchg", C.c_int32),
     ]
 
 
@@ -104,6 +106,7 @@ KERNEL_FORMS = {
     "priv_rows": {"auto": 0, "off": 1, "on": 2},
     "dp_dense": {"auto": 0, "records": 1, "partials": 2},
     "heavy_chunk": {"auto": 0, "off": 1, "on": 2},
+    "dp_xchg": {"collective": 0, "p2p": 1},
 }
 
 
@@ -161,6 +164,14 @@ def load(path: str | None = None):
         getattr(lib, fn).argtypes = [_P, C.c_int64, _P]
         getattr(lib, fn).restype = C.c_int
     for fn in ("rae_set_dp_buffers", "rae_dp_list_max"):
+        getattr(lib, fn).restype = C.c_int
+    lib.rae_ipc_export.argtypes = [_P, _P, C.POINTER(C.c_int64)]
+    lib.rae_ipc_open.argtypes = [_P, C.POINTER(_P)]
+    lib.rae_ipc_close.argtypes = [_P]
+    lib.rae_p2p_signals.argtypes = [_P]
+    lib.rae_p2p_signals.restype = _P
+    lib.rae_set_peer.argtypes = [_P, C.c_int32, _P, _P, _P, _P, _P]
+    for fn in ("rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_set_peer"):
         getattr(lib, fn).restype = C.c_int
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]

@@ -94,6 +94,13 @@ class Exchange:
         else:
             dist.all_to_all_single(recv, send, group=self.group)
 
+    def all_gather_object(self, obj):
+        """Every rank's `obj` (a picklable Python object), in rank order -- set-up only (the
+        peer-to-peer exchange's IPC handles)."""
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
     def max_int(self, v: int) -> int:
         dev = torch.device("cuda", torch.cuda.current_device()) if \
             dist.get_backend(self.group) == "nccl" else torch.device("cpu")

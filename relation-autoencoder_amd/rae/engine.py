@@ -122,6 +122,12 @@ class TrainEngine:
         self._dp = self.kernel_forms["dp_update"] == "partitioned" and self.world_size > 1
         if self._dp and exchange is None:
             raise ValueError("the partitioned data-parallel update needs the ranks' Exchange")
+        # peer-to-peer exchange (include/rae.h RAE_XCHG_P2P): the kernels store rows and
+        # records straight into the peers' IPC-mapped buffers -- no collective inside a step
+        self._p2p = self.kernel_forms.get("dp_xchg") == "p2p" and self.world_size > 1
+        if self.kernel_forms.get("dp_xchg") == "p2p" and self.kernel_forms["dp_update"] != "partitioned":
+            raise ValueError("the peer-to-peer exchange runs the partitioned update")
+        self._ipc_bases = {}         # handle bytes -> this process's mapping of a peer allocation
         for key, val in self.kernel_forms.items():
             if key not in _lib.KERNEL_FORMS or val not in _lib.KERNEL_FORMS[key]:
                 raise ValueError(f"unknown kernel form {key}={val!r}")
@@ -161,6 +167,8 @@ class TrainEngine:
         _lib.check(self.lib.rae_plan_create(C.byref(cfg), C.byref(bufs), C.byref(handle)),
                    "rae_plan_create")
         self.plan = handle
+        if self._p2p:
+            self._p2p_setup()
         self.index_window = int(self.lib.rae_index_window(self.plan))
         # a batch's row index is hash-partitioned (rae_index.hpp RAE_IDX_PART records per
         # partition) and a partition can overflow its LDS sort (a Zipf-heavy row at a large global
@@ -201,6 +209,42 @@ class TrainEngine:
         self._ready = None           # (lo, hi, negatives version, side-stream event): _mark_built
         self._neg_version = 0
 
+    # ------------------------------------------------------------------ peer-to-peer exchange
+    def _ipc_export(self, ptr: int):
+        h = (C.c_char * _lib.RAE_IPC_HANDLE_BYTES)()
+        off = C.c_int64()
+        _lib.check(self.lib.rae_ipc_export(C.c_void_p(ptr), h, C.byref(off)), "rae_ipc_export")
+        return bytes(h), int(off.value)
+
+    def _ipc_map(self, handle: bytes, offset: int) -> int:
+        base = self._ipc_bases.get(handle)
+        if base is None:
+            b = C.c_void_p()
+            _lib.check(self.lib.rae_ipc_open(C.c_char_p(handle), C.byref(b)), "rae_ipc_open")
+            base = self._ipc_bases[handle] = int(b.value)
+        return base + offset
+
+    def _p2p_setup(self):
+        """Trade IPC handles of this rank's exchange buffer, W, A, Ab and signal counters with
+        every peer (a collective over the ranks' process group, once) and hand the peers'
+        mappings to the plan (rae_set_peer).  Tensors sharing one allocation map it once."""
+        named = self._named
+        sig = self.lib.rae_p2p_signals(self.plan)
+        mine = {"ex": self._ipc_export(self.exchange_buf.data_ptr()),
+                "W": self._ipc_export(named["W"].data_ptr()),
+                "A": self._ipc_export(named["A"].data_ptr()),
+                "Ab": self._ipc_export(named["Ab"].data_ptr()),
+                "sig": self._ipc_export(int(sig))}
+        everyone = self.exchange.all_gather_object(mine)
+        for p, e in enumerate(everyone):
+            if p == self.rank:
+                continue
+            ptr = {k: self._ipc_map(*e[k]) for k in ("ex", "W", "A", "Ab", "sig")}
+            _lib.check(self.lib.rae_set_peer(self.plan, p, C.c_void_p(ptr["ex"]),
+                                             C.c_void_p(ptr["W"]), C.c_void_p(ptr["A"]),
+                                             C.c_void_p(ptr["Ab"]), C.c_void_p(ptr["sig"])),
+                       "rae_set_peer")
+
     # ------------------------------------------------------------------ partitioned update
     def _dp_caps_check(self):
         """After a row-index build: the longest peer row list of the batches just built,
@@ -211,18 +255,23 @@ class TrainEngine:
         need_a = self.exchange.max_int(ma.value)
         need_w = self.exchange.max_int(mw.value)
         ca, cw = self._dp_caps or (0, 0)
-        if self._dp_send is not None and need_a <= ca and need_w <= cw:
+        if self._dp_caps is not None and need_a <= ca and need_w <= cw:
             return
         # headroom: the first window's longest list is already the tail of many batches, and
         # a longer one later only re-sizes (a one-off): every padded row travels every step
         ca = min(max(ca, int(need_a * 1.04) + 16), self._dp_cap_max[0])
         cw = min(max(cw, int(need_w * 1.04) + 16), self._dp_cap_max[1])
-        blk = int(self.lib.rae_dp_block_floats(C.byref(self.cfg), ca, cw))
-        self._dp_send = torch.zeros(self.world_size * blk, dtype=torch.float32, device=self.device)
-        self._dp_recv = torch.zeros_like(self._dp_send)
-        _lib.check(self.lib.rae_set_dp_buffers(self.plan, C.c_void_p(self._dp_send.data_ptr()),
-                                               C.c_void_p(self._dp_recv.data_ptr()), ca, cw),
-                   "rae_set_dp_buffers")
+        if self._p2p:                # capacities only: rows go straight into the peers' replicas
+            _lib.check(self.lib.rae_set_dp_buffers(self.plan, None, None, ca, cw),
+                       "rae_set_dp_buffers")
+        else:
+            blk = int(self.lib.rae_dp_block_floats(C.byref(self.cfg), ca, cw))
+            self._dp_send = torch.zeros(self.world_size * blk, dtype=torch.float32,
+                                        device=self.device)
+            self._dp_recv = torch.zeros_like(self._dp_send)
+            _lib.check(self.lib.rae_set_dp_buffers(self.plan, C.c_void_p(self._dp_send.data_ptr()),
+                                                   C.c_void_p(self._dp_recv.data_ptr()), ca, cw),
+                       "rae_set_dp_buffers")
         self._dp_caps = (ca, cw)
         self._graphs.clear()
 
@@ -263,6 +312,9 @@ class TrainEngine:
             self._graphs.clear()
             self.lib.rae_plan_destroy(self.plan)
             self.plan = None
+            for base in self._ipc_bases.values():
+                self.lib.rae_ipc_close(C.c_void_p(base))
+            self._ipc_bases = {}
 
     def __del__(self):
         try:
@@ -297,6 +349,8 @@ class TrainEngine:
         res["priv_rows"] = name["priv_rows"][out.priv_rows]
         if sp and self.world_size > 1:
             res["dp_dense"] = name["dp_dense"][out.dp_dense]
+        if self.world_size > 1:
+            res["dp_xchg"] = name["dp_xchg"][out.dp_xchg]
         res["heavy_chunk"] = name["heavy_chunk"][out.heavy_chunk]
         return res
 
@@ -403,7 +457,7 @@ class TrainEngine:
         given) at absolute batches first, first+1, ... (the cursor is not touched: every
         cursor-driven run sets it first)."""
         for i in range(count):
-            if self._dp:                     # pull the rows this step's examples read
+            if self._dp and not self._p2p:   # pull the rows this step's examples read
                 if first is None:
                     _lib.check(self.lib.rae_dp_pack(self.plan, i, st), "rae_dp_pack")
                 else:
@@ -419,7 +473,7 @@ class TrainEngine:
             else:
                 _lib.check(self.lib.rae_step_forward_at(self.plan, first + i, st),
                            "rae_step_forward_at")
-            if self.exchange is not None:
+            if self.exchange is not None and not self._p2p:
                 self.exchange(self.exchange_buf)
             if first is None:
                 _lib.check(self.lib.rae_step_update(self.plan, i, st), "rae_step_update")

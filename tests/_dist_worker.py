@@ -185,7 +185,8 @@ def run_sync_rows(out):
     np.savez(os.path.join(out, f"rows_{rk}.npz"), recv=recv.numpy(), t2=t2.numpy(), t1=t1.numpy())
 
 
-def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", index_window=0):
+def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", index_window=0,
+            xchg="collective", graph_chunk=1):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -196,19 +197,22 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", ind
     ex = rdist.make_exchange(ws, rk)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), DP_SHAPE["epochs"], 0.1, l, r,
                              m, s, 0.0, 0.0, "adagrad", "dp", decoder, False, True, False, 1.0,
-                             device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
-                             dp_update=dp_update,
+                             device=dev, world_size=ws, rank=rk, exchange=ex,
+                             graph_chunk=graph_chunk, dp_update=dp_update,
                              kernel_forms=dict({"dp_dense": dense} if decoder == "sp" else {},
-                                               priv_rows=priv),
+                                               priv_rows=priv, dp_xchg=xchg),
                              index_window=index_window)
     ind.learn(verbose=False)
+    if xchg == "p2p":
+        assert ind.engine.kernel_forms_in_use()["dp_xchg"] == "p2p"
     if decoder == "sp" and dense != "auto":
         assert ind.engine.kernel_forms_in_use()["dp_dense"] == dense
     if priv != "auto":
         assert ind.engine.kernel_forms_in_use()["priv_rows"] == priv
     ind.engine.sync_replicas()
     params = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
-    np.savez(os.path.join(out, f"gpu_{dp_update}_{decoder}_{rk}.npz"),
+    tag = dp_update if xchg == "collective" else f"{dp_update}_{xchg}"
+    np.savez(os.path.join(out, f"gpu_{tag}_{decoder}_{rk}.npz"),
              costs=np.concatenate(ind.epoch_costs), **params)
 
 
@@ -252,6 +256,9 @@ def c4dp_dataset():
 
 
 def run_gpu_c4dp(out, dp_update="replicated"):
+    xchg = "collective"
+    if dp_update == "p2p":               # the partitioned update over the peer-to-peer exchange
+        dp_update, xchg = "partitioned", "p2p"
     """BASELINE config 4's model shape (K = 300, embed 300, neg 50, l = 100 per rank) on a
     reduced synthetic set: the data-parallel kernels the 8-GPU config runs together -- the split
     SP forward (r m > 32768), the wire records with every example's dw1 / dw2 (dp_dense records
@@ -268,11 +275,12 @@ def run_gpu_c4dp(out, dp_update="replicated"):
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, c["l"], c["r"], c["m"],
                              c["s"], 0.0, 0.0, "adagrad", "c4dp", "sp", False, True, False, 1.0,
                              device=dev, world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
-                             dp_update=dp_update)
+                             dp_update=dp_update, kernel_forms={"dp_xchg": xchg})
     ind.compile_function()
     eng = ind.engine
     forms = eng.kernel_forms_in_use()
-    want = {"sp_forward": "split", "dp_update": dp_update, "priv_rows": "off", "dp_dense": "records"}
+    want = {"sp_forward": "split", "dp_update": dp_update, "priv_rows": "off", "dp_dense": "records",
+            "dp_xchg": xchg}
     assert {k: forms[k] for k in want} == want, forms
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
     snap = {}
@@ -283,7 +291,7 @@ def run_gpu_c4dp(out, dp_update="replicated"):
         eng.sync_replicas()
         for k, v in ind.modelFunc.named_params().items():
             snap[f"{k}@{b}"] = v.detach().cpu().numpy()
-    np.savez(os.path.join(out, f"c4dp_{dp_update}_{rk}.npz"),
+    np.savez(os.path.join(out, f"c4dp_{dp_update if xchg == 'collective' else 'p2p'}_{rk}.npz"),
              costs=eng.costs[:c["steps"]].cpu().numpy(), **snap)
 
 
@@ -407,7 +415,9 @@ def main():
             run_gpu(out, dec, sys.argv[4] if len(sys.argv) > 4 else "replicated",
                     sys.argv[5] if len(sys.argv) > 5 else "auto",
                     sys.argv[6] if len(sys.argv) > 6 else "auto",
-                    int(sys.argv[7]) if len(sys.argv) > 7 else 0)
+                    int(sys.argv[7]) if len(sys.argv) > 7 else 0,
+                    sys.argv[8] if len(sys.argv) > 8 else "collective",
+                    int(sys.argv[9]) if len(sys.argv) > 9 else 1)
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
                        heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")

@@ -236,7 +236,8 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
     """BASELINE config 4's data-parallel kernel combination -- K = 300,
     embed 300, neg 50, l = 100 per rank: the split SP forward, the wire records (dw1 / dw2 per
     example), k_vrec and 102 record slots with private rows off -- on `ws` ranks sharing the GPU
-    (gloo), both update forms (the worker asserts the resolved forms).  Checked:
+    (gloo), both update forms, the partitioned one also over the peer-to-peer exchange (the
+    worker asserts the resolved forms).  Checked:
       * replicas bit-identical, partitioned == replicated bitwise;
       * == the float64 oracle at the global batch (fp32 tolerance);
       * == a single-rank plan at the global batch, whose split forward writes V1 / V2 / G1 into
@@ -244,9 +245,11 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
         (k_vrec) and the update sums them in the same order."""
     _launch(["gpu_c4dp", str(tmp_path), "replicated"], nproc=ws, timeout=600)
     _launch(["gpu_c4dp", str(tmp_path), "partitioned"], nproc=ws, timeout=600)
+    _launch(["gpu_c4dp", str(tmp_path), "p2p"], nproc=ws, timeout=600)
     want_c, want_p, (single_p, single_c) = _c4dp_reference(cuda_dev, ws)
     gr = [np.load(tmp_path / f"c4dp_replicated_{k}.npz") for k in range(ws)]
-    gp = [np.load(tmp_path / f"c4dp_partitioned_{k}.npz") for k in range(ws)]
+    gp = [np.load(tmp_path / f"c4dp_partitioned_{k}.npz") for k in range(ws)] + \
+        [np.load(tmp_path / f"c4dp_p2p_{k}.npz") for k in range(ws)]
     last = C4DP_SHAPE["steps"] - 1
     for g in gr[1:] + gp:
         np.testing.assert_array_equal(g["costs"], gr[0]["costs"])
@@ -259,3 +262,32 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
     np.testing.assert_array_equal(gr[0]["costs"], single_c)
     diff = {k: int(np.sum(gr[0][k] != single_p[k])) for k in sorted(single_p)}
     assert not any(diff.values()), f"data-parallel vs single-rank elements differing: {diff}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decoder,ws,graph_chunk,iw", [("sp", 2, 1, 0), ("sp", 4, 4, 0),
+                                                       ("rescal", 2, 1, 0), ("rescal+sp", 4, 1, 0),
+                                                       ("sp", 8, 4, 0), ("sp", 2, 2, 4)])
+def test_gpu_p2p_exchange(built_lib, cuda_dev, tmp_path, decoder, ws, graph_chunk, iw):
+    """the partitioned update over the peer-to-peer exchange (include/rae.h
+    RAE_XCHG_P2P, csrc/rae_p2p.hpp) -- owners store the rows each peer's next batch reads into
+    the peer's IPC-mapped replica, every forward stores its records into every peer's exchange
+    buffer, and the kernels wait on the peers' system-scope signal counters -- on `ws` ranks
+    sharing the GPU, eager (graph_chunk 1) and graph-replayed (no collective inside a step, so
+    the steps capture under gloo too), iw = 4: a ring of four batches (many windows, the row-list
+    capacities agreed per window).  == the collective replicated update bitwise (costs and
+    parameters), replicas bit-identical after the final gather, == the float64 oracle."""
+    _launch(["gpu", str(tmp_path), decoder, "partitioned", "auto", "auto", str(iw), "p2p",
+             str(graph_chunk)], nproc=ws, timeout=420)
+    _launch(["gpu", str(tmp_path), decoder, "replicated", "auto", "auto", str(iw)], nproc=ws)
+    tr, costs = _single_process_oracle(decoder, ws=ws)
+    gp = [np.load(tmp_path / f"gpu_partitioned_p2p_{decoder}_{k}.npz") for k in range(ws)]
+    gr = np.load(tmp_path / f"gpu_replicated_{decoder}_0.npz")
+    np.testing.assert_array_equal(gp[0]["costs"], gr["costs"])
+    np.testing.assert_allclose(gp[0]["costs"], costs, rtol=2e-5, atol=2e-5)
+    for k, v in tr.params.items():
+        for g in gp[1:]:
+            np.testing.assert_array_equal(gp[0][k], g[k])
+        np.testing.assert_array_equal(gp[0][k], gr[k])
+        err = np.abs(gp[0][k] - v)
+        assert np.all(err <= 2e-4 + 2e-3 * np.abs(v)), f"{k}: max err {err.max():.3e}"
