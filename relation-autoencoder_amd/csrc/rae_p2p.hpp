@@ -103,7 +103,9 @@ __device__ void p2p_wait(const StepArgs& a, int kind, unsigned per) {
     const unsigned target = *ex + per;
     const unsigned* s = a.sig + kind * a.G + p;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)(__hip_atomic_load(s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+    // a wait that already timed out this run: do not wait again (fail fast; rae_check raises)
+    const bool dead = (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 64) != 0;
+    while (!dead && (int)(__hip_atomic_load(s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > RAE_P2P_TIMEOUT) {
             atomicOr(a.err, 64);
             break;
