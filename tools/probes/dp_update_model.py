@@ -10,6 +10,11 @@ Times, per step, with the kernels' own dispatch timestamps (rae_time_next):
   replicated   rank 0 of a G-rank plan: forward (l examples), update over the global batch
                L = G*l (with the SP wire record: k_vrec + k_update), row index of the global batch;
   partitioned  the same with the row-owner partitioned update: + the row pull's pack / unpack.
+  p2p          the partitioned update over the peer-to-peer exchange (include/rae.h RAE_XCHG_P2P):
+               the row and record pushes and the signal waits are kernels of the step; here the
+               "peers" are local dummy buffers and the signal words loop back to this rank's own
+               counters (a push's signals are the waits' expected counts), so the pushes' stores
+               and the waits' polling are timed, the link is not.
 Whole steps as the epoch loop runs them (graph replays of n steps, HIP events): alone
 ("graph_step") and with the next n batches' row index built beside them on the side stream
 ("graph_step_with_index": engine index_overlap).
@@ -49,17 +54,40 @@ class NoPeers:
         pass
 
 
+def loopback_p2p_setup(eng):
+    """Peers of a G-rank plan with no peer processes: every peer's exchange buffer / replica
+    is one local dummy buffer set, and peer p's signal words start (p - rank) words before this
+    rank's, so the push's add on "peer p's word (kind, rank)" lands on this rank's word
+    (kind, p) -- the count the wait for peer p expects."""
+    import torch
+    named = eng._named
+    eng._loop = [torch.zeros_like(eng.exchange_buf), torch.empty_like(named["W"]),
+                 torch.empty_like(named["A"]), torch.empty_like(named["Ab"])]
+    sig = int(eng.lib.rae_p2p_signals(eng.plan))
+    for p in range(eng.world_size):
+        if p != eng.rank:
+            ex, W, A, Ab = (C.c_void_p(t.data_ptr()) for t in eng._loop)
+            rc = eng.lib.rae_set_peer(eng.plan, p, ex, W, A, Ab, C.c_void_p(sig + 4 * (p - eng.rank)))
+            assert rc == 0, eng.lib.rae_last_error()
+
+
 def measure(args, cfg, data, gold, G, mode):
     import torch
+    from rae import engine as E
     from rae.inducer import ReconstructInducer
     dev = torch.device("cuda", 0)
+    forms = dict(kv.split("=", 1) for kv in args.kernel_form) if G > 1 else {}
+    p2p = mode == "p2p"
+    if p2p:
+        mode = "partitioned"
+        forms["dp_xchg"] = "p2p"
+        E.TrainEngine._p2p_setup = loopback_p2p_setup
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
                              cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
                              True, False, 1.0, device=dev, world_size=G, rank=0,
                              exchange=NoPeers(G) if G > 1 else None, graph_chunk=args.graph_n,
                              mfma_bf16=cfg.get("bf16", False), dp_update=mode,
-                             kernel_forms=dict(kv.split("=", 1) for kv in args.kernel_form)
-                             if G > 1 else None)
+                             kernel_forms=forms or None)
     ind.compile_function()
     eng = ind.engine
     eng.sample_epoch_negatives(ind.negativeSampler, "device")
@@ -84,7 +112,7 @@ def measure(args, cfg, data, gold, G, mode):
         h = C.c_void_p()
         assert lib.rae_event_create(C.byref(h)) == 0
         return h
-    part = mode == "partitioned" and G > 1
+    part = mode == "partitioned" and G > 1 and not p2p
     t = {"forward": [], "update": []}
     if part:
         t.update(pack=[], unpack=[])
@@ -112,11 +140,14 @@ def measure(args, cfg, data, gold, G, mode):
     out["record_floats"] = eng.rec_floats
     if G > 1:
         out["records_allgather_in_bytes"] = (G - 1) * args.l * eng.rec_floats * 4
-    if part:
+    if part or p2p:
         ca, cw = eng._dp_caps
         blk = int(lib.rae_dp_block_floats(C.byref(eng.cfg), ca, cw)) * 4
         out["rows_alltoall_in_bytes"] = (G - 1) * blk
         out["row_caps"] = [ca, cw]
+    if p2p:
+        out["xchg"] = "p2p (forward = row push + wait + forward + record push; update = wait + "\
+                      "update)"
     out["kernel_forms"] = eng.kernel_forms_in_use()
     out.update(graph_steps(eng, args))
     ind._drop_engine()
@@ -155,6 +186,23 @@ def graph_steps(eng, args):
             "graph_step_with_index": float(np.median(ovl))}
 
 
+def project_p2p(r, t1, args):
+    """The peer-to-peer step: the measured graph step (its pushes' local stores and the waits'
+    polling included) + whatever of each push's inbound bytes the link cannot move while the
+    push kernel runs + one signal latency per exchange (a system-scope release seen by the
+    peer's poll over xGMI)."""
+    bw = args.links * args.link_gbs * args.eff * 1e3          # bytes per us
+    tg = r["graph_step_with_index"]
+    rec_t = r["records_allgather_in_bytes"] / bw
+    row_t = r["rows_alltoall_in_bytes"] / bw
+    extra = max(0.0, rec_t - args.push_us) + max(0.0, row_t - args.push_us) + 2 * args.p2p_lat_us
+    return {"step_us": tg + extra, "kernels_us": tg, "link_and_signal_us": extra,
+            "records_in_us": rec_t, "rows_in_us": row_t, "efficiency": t1 / (tg + extra),
+            "efficiency_if_link_free": t1 / tg,
+            "model": "graph step (pushes + waits local) + max(0, inbound bytes / rate - "
+                     "push_us) per push + 2 signal latencies"}
+
+
 def project(res, args):
     bw = args.links * args.link_gbs * args.eff * 1e3          # bytes per us
     coll = lambda b: args.lat_us + b / bw                      # noqa: E731
@@ -167,6 +215,10 @@ def project(res, args):
                             "model": "step = graph-replayed step with the index built beside "
                                      "it (measured) + A2A (partitioned) + AG, every collective "
                                      "lat + bytes / inbound rate, not overlapped"}}
+    if res.get("p2p"):
+        proj["p2p"] = project_p2p(res["p2p"], t1, args)
+        proj["assumptions"]["p2p_signal_latency_us"] = args.p2p_lat_us
+        proj["assumptions"]["push_overlap_us"] = args.push_us
     for mode in ("replicated", "partitioned"):
         r = res.get(mode)
         if not r:
@@ -193,7 +245,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--graph-n", type=int, default=64, help="steps per timed graph replay")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="replicated,partitioned")
+    ap.add_argument("--modes", default="replicated,partitioned,p2p")
     ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
                     help="kernel form of the G-rank plans (e.g. priv_rows=off)")
     ap.add_argument("--link-gbs", type=float, default=76.8,
@@ -201,6 +253,11 @@ def main():
     ap.add_argument("--links", type=int, default=7)
     ap.add_argument("--eff", type=float, default=0.7, help="achievable fraction of the links")
     ap.add_argument("--lat-us", type=float, default=10.0, help="per-collective latency")
+    ap.add_argument("--p2p-lat-us", type=float, default=3.0,
+                    help="peer-to-peer signal latency (release -> the peer's poll sees it)")
+    ap.add_argument("--push-us", type=float, default=0.0,
+                    help="link time hidden under each push kernel (its own measured duration "
+                         "is in the graph step)")
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     data, gold = synthetic_dataset(cfg["N"], cfg["d"], cfg["ntrue"], seed=1234)
