@@ -39,8 +39,10 @@ using namespace rae;
 
 #define RAE_VERSION 1
 #ifndef RAE_P2P_GRID
-#define RAE_P2P_GRID 256      // workgroups of a peer-to-peer push (each signals every peer)
+#define RAE_P2P_GRID 16       // workgroups of a peer-to-peer push: each ends with a system-scope
+                              // release (an L2 write-back) and one signal per peer
 #endif
+#define RAE_P2P_BT 1024       // threads per push workgroup
 #ifndef RAE_UPD_WPE
 #define RAE_UPD_WPE 5   // SP update: <= 102 VGPRs -> 20 waves per CU (6: 85 VGPRs spilled the
                         // Q = 2 rows of C4 -- 23.8 vs 20.2 us update; r03_ab.txt)
@@ -206,8 +208,8 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_dplists(StepArgs a, int64_t f
                            smem);
 }
 // peer-to-peer exchange (rae_p2p.hpp)
-__global__ __launch_bounds__(RAE_BT) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
-__global__ __launch_bounds__(RAE_BT) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
+__global__ __launch_bounds__(1024) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
+__global__ __launch_bounds__(1024) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
 __global__ __launch_bounds__(64) void k_p2p_wait(StepArgs a, int kind, unsigned per) {
     p2p_wait(a, kind, per);
 }
@@ -710,9 +712,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
                                    "priv_rows / dp_dense / heavy_chunk / dp_xchg)");
-    if (c.dp_xchg == RAE_XCHG_P2P && (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31))
+    if (c.dp_xchg == RAE_XCHG_P2P && (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31 ||
+                                      c.embed % 4 || c.relations % 4 || c.embed > 512 ||
+                                      c.relations > 512))
         return fail(RAE_E_INVALID, "the peer-to-peer exchange runs the partitioned update "
-                                   "(world_size <= 31)");
+                                   "(world_size <= 31; embed and relations multiples of 4, <= 512)");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -1227,13 +1231,13 @@ static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st) {
 
 // peer-to-peer exchange grids (every rank the same: the peers expect these many signals)
 static unsigned p2p_rows_grid(const StepArgs& a) {
-    const int64_t waves = (int64_t)a.G * (a.capA + a.capW);
-    const int64_t g = (waves + RAE_NWAVE - 1) / RAE_NWAVE;
+    const int64_t rounds = ((int64_t)a.G * (a.capA + a.capW) + RAE_P2P_RPW - 1) / RAE_P2P_RPW;
+    const int64_t g = (rounds + RAE_P2P_BT / 64 - 1) / (RAE_P2P_BT / 64);
     return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
 }
 static unsigned p2p_recs_grid(const StepArgs& a) {
     const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;
-    const int64_t g = (n4 + RAE_BT - 1) / RAE_BT;
+    const int64_t g = (n4 + RAE_P2P_BT - 1) / RAE_P2P_BT;
     return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
 }
 static bool p2p_on(const rae_plan* p) { return p->args.xchg == RAE_XCHG_P2P && p->args.G > 1; }
@@ -1248,7 +1252,7 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     if (p2p) {                // the owned rows the peers' examples read, into their replicas
         if (!p->peers_set) return fail(RAE_E_STATE, "peer buffers not set (rae_set_peer)");
         const unsigned gr = p2p_rows_grid(a);
-        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_P2P_BT), 0, st, a);
         RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, gr);
     }
     if (a.dec == RAE_DEC_SP) {
@@ -1259,7 +1263,7 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     else if (p->v4) launch_fwd_bil<true>(p, a, st);
     else launch_fwd_bil<false>(p, a, st);
     if (p2p)                  // this rank's records into every peer's exchange buffer
-        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_P2P_BT), 0, st, a);
     p->t_start = p->t_stop = nullptr;
     HIPCHK(hipGetLastError());
     return RAE_OK;

@@ -64,33 +64,57 @@ __device__ void p2p_push_records(const StepArgs& a) {
     p2p_signal(a, 0);
 }
 
-// k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
-// this rank owns that the peer's examples read): the row into the peer's replica
+// k_p2p_rows: waves grid-stride over (peer, list entry) of batch step_batch(a)'s direction-0
+// lists (rows this rank owns that the peer's examples read), RAE_P2P_RPW entries per round with
+// every row load issued before the stores: each row into that peer's replica
+#define RAE_P2P_RPW 4
 __device__ void p2p_push_rows(const StepArgs& a) {
     const int lane = threadIdx.x & 63;
     const int per = a.capA + a.capW;
     const int64_t slot = step_batch(a) % a.index_window;
-    for (int64_t t = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-         t < (int64_t)a.G * per; t += (int64_t)gridDim.x * (blockDim.x / 64)) {
-        const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
-        if (p == a.rank) continue;
-        const int tab = i0 >= a.capA ? 1 : 0;
-        const int i = tab ? i0 - a.capA : i0;
-        const int cap = tab ? a.capW : a.capA;
-        const int n = *dpl_count(a, slot, 0, p, tab);
-        if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
-        if (i >= n || i >= cap) continue;
-        const int row = dpl_list(a, slot, 0, p, tab)[i];
-        const int w = tab ? a.m : a.r;
-        const float* s = (tab ? a.W : a.A) + (int64_t)row * w;
-        float* d = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;
-        if ((w & 3) == 0) {
-            for (int c = lane; c < w / 4; c += RAE_WAVE)
-                reinterpret_cast<float4*>(d)[c] = reinterpret_cast<const float4*>(s)[c];
-        } else {
-            for (int c = lane; c < w; c += RAE_WAVE) d[c] = s[c];
+    const int64_t nt = (int64_t)a.G * per;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t t0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * RAE_P2P_RPW;
+         t0 < nt; t0 += nw * RAE_P2P_RPW) {
+        float4 v[RAE_P2P_RPW][2];                    // rows of up to 128 float4
+        float ab[RAE_P2P_RPW];
+        float* dst[RAE_P2P_RPW];
+        float* dab[RAE_P2P_RPW];
+        int w4[RAE_P2P_RPW];
+#pragma unroll
+        for (int u = 0; u < RAE_P2P_RPW; ++u) {
+            dst[u] = nullptr;
+            dab[u] = nullptr;
+            w4[u] = 0;
+            const int64_t t = t0 + u;
+            if (t >= nt) continue;
+            const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
+            if (p == a.rank) continue;
+            const int tab = i0 >= a.capA ? 1 : 0;
+            const int i = tab ? i0 - a.capA : i0;
+            const int cap = tab ? a.capW : a.capA;
+            const int n = *dpl_count(a, slot, 0, p, tab);
+            if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
+            if (i >= n || i >= cap) continue;
+            const int row = dpl_list(a, slot, 0, p, tab)[i];
+            const int w = tab ? a.m : a.r;              // r, m multiples of 4, <= 512
+            w4[u] = w / 4;
+            const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
+            dst[u] = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;
+            if (lane < w4[u]) v[u][0] = s[lane];
+            if (lane + 64 < w4[u]) v[u][1] = s[lane + 64];
+            if (!tab) {
+                ab[u] = a.Ab[row];
+                dab[u] = a.peers[p].Ab + row;
+            }
         }
-        if (!tab && lane == 0) a.peers[p].Ab[row] = a.Ab[row];
+#pragma unroll
+        for (int u = 0; u < RAE_P2P_RPW; ++u) {
+            if (!dst[u]) continue;
+            if (lane < w4[u]) reinterpret_cast<float4*>(dst[u])[lane] = v[u][0];
+            if (lane + 64 < w4[u]) reinterpret_cast<float4*>(dst[u])[lane + 64] = v[u][1];
+            if (dab[u] && lane == 0) *dab[u] = ab[u];
+        }
     }
     p2p_signal(a, 1);
 }
