@@ -38,11 +38,6 @@
 using namespace rae;
 
 #define RAE_VERSION 1
-#ifndef RAE_P2P_GRID
-#define RAE_P2P_GRID 16       // workgroups of a peer-to-peer push: each ends with a system-scope
-                              // release (an L2 write-back) and one signal per peer
-#endif
-#define RAE_P2P_BT 1024       // threads per push workgroup
 #ifndef RAE_UPD_WPE
 #define RAE_UPD_WPE 5   // SP update: <= 102 VGPRs -> 20 waves per CU (6: 85 VGPRs spilled the
                         // Q = 2 rows of C4 -- 23.8 vs 20.2 us update; r03_ab.txt)
@@ -208,8 +203,9 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_dplists(StepArgs a, int64_t f
                            smem);
 }
 // peer-to-peer exchange (rae_p2p.hpp)
-__global__ __launch_bounds__(1024) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
-__global__ __launch_bounds__(1024) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
+__global__ __launch_bounds__(RAE_BT) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
+__global__ __launch_bounds__(RAE_BT) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
+__global__ __launch_bounds__(64) void k_p2p_signal(StepArgs a, int kind) { p2p_signal(a, kind); }
 __global__ __launch_bounds__(64) void k_p2p_wait(StepArgs a, int kind, unsigned per) {
     p2p_wait(a, kind, per);
 }
@@ -1231,14 +1227,12 @@ static void launch_fwd_dp(rae_plan* p, const StepArgs& a, hipStream_t st) {
 
 // peer-to-peer exchange grids (every rank the same: the peers expect these many signals)
 static unsigned p2p_rows_grid(const StepArgs& a) {
-    const int64_t rounds = ((int64_t)a.G * (a.capA + a.capW) + RAE_P2P_RPW - 1) / RAE_P2P_RPW;
-    const int64_t g = (rounds + RAE_P2P_BT / 64 - 1) / (RAE_P2P_BT / 64);
-    return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
+    const int64_t g = ((int64_t)a.G * (a.capA + a.capW) + RAE_NWAVE - 1) / RAE_NWAVE;
+    return (unsigned)(g < 1 ? 1 : g);
 }
 static unsigned p2p_recs_grid(const StepArgs& a) {
-    const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;
-    const int64_t g = (n4 + RAE_P2P_BT - 1) / RAE_P2P_BT;
-    return (unsigned)(g < 1 ? 1 : (g > RAE_P2P_GRID ? RAE_P2P_GRID : g));
+    const int64_t g = ((int64_t)a.l * a.lay.rec / 4 + RAE_BT - 1) / RAE_BT;
+    return (unsigned)(g < 1 ? 1 : g);
 }
 static bool p2p_on(const rae_plan* p) { return p->args.xchg == RAE_XCHG_P2P && p->args.G > 1; }
 
@@ -1251,9 +1245,10 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     const bool p2p = p2p_on(p);
     if (p2p) {                // the owned rows the peers' examples read, into their replicas
         if (!p->peers_set) return fail(RAE_E_STATE, "peer buffers not set (rae_set_peer)");
-        const unsigned gr = p2p_rows_grid(a);
-        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_P2P_BT), 0, st, a);
-        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, gr);
+        const unsigned gr = p2p_rows_grid(a);     // (>= 1 workgroup: the signal follows anyway)
+        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 1);
+        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, 1u);
     }
     if (a.dec == RAE_DEC_SP) {
         launch_fwd_sp(p, a, st);
@@ -1263,7 +1258,10 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     else if (p->v4) launch_fwd_bil<true>(p, a, st);
     else launch_fwd_bil<false>(p, a, st);
     if (p2p)                  // this rank's records into every peer's exchange buffer
-        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_P2P_BT), 0, st, a);
+    {
+        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_BT), 0, st, a);
+        RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 0);
+    }
     p->t_start = p->t_stop = nullptr;
     HIPCHK(hipGetLastError());
     return RAE_OK;
@@ -1325,7 +1323,7 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     a.stamps = p->stamps_upd;
     const dim3 gu(p->grid_update), bt(RAE_BT);
     if (p2p_on(p))            // every peer's records of this batch are here
-        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 0, p2p_recs_grid(a));
+        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 0, 1u);
     if (a.lay.wire)           // the vectors the wire records left out, for the whole batch
     {
         const dim3 gv(ceil_div(vrec_tasks(a.L, a.r), RAE_NWAVE));

@@ -14,9 +14,10 @@
 //   k_p2p_recs   its l records into every peer's exchange buffer, at the same rows
 //   k_p2p_wait   (records): until every peer's records of batch b are here
 //   update(b)    the owned rows, as before
-// Signalling: a pushing workgroup's stores are fenced at system scope, then one system-scope
-// atomic add per peer on the peer's signal word (kind, this rank) -- a counter that grows by the
-// push grid's workgroups every step.  The waiting kernel (one wave: lane p watches peer p) spins
+// Signalling: after a push kernel (its stores released at the kernel boundary) a one-wave
+// signal kernel fences at system scope and adds one to the peer's signal word (kind, this rank)
+// with a system-scope release -- a counter that grows by one every step (fences per workgroup
+// inside the pushes cost an L2 write-back each: 55-81 us per step in the loopback model).  The waiting kernel (one wave: lane p watches peer p) spins
 // on acquire loads until each counter reaches its expected value (kept in this rank's private
 // words, advanced by the wait kernel itself, so graph replays stay in step), with a bounded spin:
 // after RAE_P2P_TIMEOUT it sets error bit 64 and returns (the host sees it at rae_check) rather
@@ -39,87 +40,61 @@ namespace rae {
 #define RAE_P2P_TIMEOUT 500000000ull   // s_memrealtime ticks (100 MHz): 5 s
 #endif
 
-// after a workgroup's peer stores: fence them at system scope, then count this workgroup into
-// every peer's signal word (kind, rank)
-__device__ __forceinline__ void p2p_signal(const StepArgs& a, int kind) {
+// k_p2p_signal (one wave, after a push kernel): the push's stores were released at the kernel
+// boundary (on gfx950 an agent-scope release writes the L2s back, every XCD's); this fences at
+// system scope once more and counts one signal into every peer's word (kind, rank)
+__device__ void p2p_signal(const StepArgs& a, int kind) {
     __threadfence_system();
-    __syncthreads();
     if (threadIdx.x < a.G && threadIdx.x != a.rank) {
         unsigned* s = a.peers[threadIdx.x].sig + kind * a.G + a.rank;
         __hip_atomic_fetch_add(s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-// k_p2p_recs: this rank's l records (float4 slices, grid-strided) into every peer's buffer
+// k_p2p_recs: this rank's l records (float4 slices) into every peer's buffer
 __device__ void p2p_push_records(const StepArgs& a) {
     const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;                 // rec is a multiple of 4
     const int64_t o4 = (int64_t)a.rank * a.l * a.lay.rec / 4;
-    const float4* src = reinterpret_cast<const float4*>(a.ex) + o4;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 v = src[i];
-        for (int p = 0; p < a.G; ++p)
-            if (p != a.rank) reinterpret_cast<float4*>(a.peers[p].ex)[o4 + i] = v;
-    }
-    p2p_signal(a, 0);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const float4 v = reinterpret_cast<const float4*>(a.ex)[o4 + i];
+    for (int p = 0; p < a.G; ++p)
+        if (p != a.rank) reinterpret_cast<float4*>(a.peers[p].ex)[o4 + i] = v;
 }
 
-// k_p2p_rows: waves grid-stride over (peer, list entry) of batch step_batch(a)'s direction-0
-// lists (rows this rank owns that the peer's examples read), RAE_P2P_RPW entries per round with
-// every row load issued before the stores: each row into that peer's replica
-#define RAE_P2P_RPW 4
+// k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
+// this rank owns that the peer's examples read): the row into that peer's replica
 __device__ void p2p_push_rows(const StepArgs& a) {
     const int lane = threadIdx.x & 63;
     const int per = a.capA + a.capW;
+    const int64_t t = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
+    if (p >= a.G || p == a.rank) return;
     const int64_t slot = step_batch(a) % a.index_window;
-    const int64_t nt = (int64_t)a.G * per;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
-    for (int64_t t0 = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * RAE_P2P_RPW;
-         t0 < nt; t0 += nw * RAE_P2P_RPW) {
-        float4 v[RAE_P2P_RPW][2];                    // rows of up to 128 float4
-        float ab[RAE_P2P_RPW];
-        float* dst[RAE_P2P_RPW];
-        float* dab[RAE_P2P_RPW];
-        int w4[RAE_P2P_RPW];
-#pragma unroll
-        for (int u = 0; u < RAE_P2P_RPW; ++u) {
-            dst[u] = nullptr;
-            dab[u] = nullptr;
-            w4[u] = 0;
-            const int64_t t = t0 + u;
-            if (t >= nt) continue;
-            const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
-            if (p == a.rank) continue;
-            const int tab = i0 >= a.capA ? 1 : 0;
-            const int i = tab ? i0 - a.capA : i0;
-            const int cap = tab ? a.capW : a.capA;
-            const int n = *dpl_count(a, slot, 0, p, tab);
-            if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
-            if (i >= n || i >= cap) continue;
-            const int row = dpl_list(a, slot, 0, p, tab)[i];
-            const int w = tab ? a.m : a.r;              // r, m multiples of 4, <= 512
-            w4[u] = w / 4;
-            const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
-            dst[u] = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;
-            if (lane < w4[u]) v[u][0] = s[lane];
-            if (lane + 64 < w4[u]) v[u][1] = s[lane + 64];
-            if (!tab) {
-                ab[u] = a.Ab[row];
-                dab[u] = a.peers[p].Ab + row;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < RAE_P2P_RPW; ++u) {
-            if (!dst[u]) continue;
-            if (lane < w4[u]) reinterpret_cast<float4*>(dst[u])[lane] = v[u][0];
-            if (lane + 64 < w4[u]) reinterpret_cast<float4*>(dst[u])[lane + 64] = v[u][1];
-            if (dab[u] && lane == 0) *dab[u] = ab[u];
-        }
-    }
-    p2p_signal(a, 1);
+    const int tab = i0 >= a.capA ? 1 : 0;
+    const int i = tab ? i0 - a.capA : i0;
+    const int cap = tab ? a.capW : a.capA;
+    // the list length and the entry load together (one round trip; the list's storage holds
+    // LA / LW >= cap entries, so entry i < cap is in bounds -- used only when i < n)
+    const int n = *dpl_count(a, slot, 0, p, tab);
+    const int row = dpl_list(a, slot, 0, p, tab)[i < cap ? i : 0];
+    if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
+    if (i >= n || i >= cap) return;
+    const int w = tab ? a.m : a.r;                   // r, m multiples of 4, <= 512
+    const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
+    float4* d = reinterpret_cast<float4*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
+    const int w4 = w / 4;
+    float4 v0, v1;
+    if (lane < w4) v0 = s[lane];
+    if (lane + 64 < w4) v1 = s[lane + 64];
+    const float ab = (!tab && lane == 0) ? a.Ab[row] : 0.f;
+    if (lane < w4) d[lane] = v0;
+    if (lane + 64 < w4) d[lane + 64] = v1;
+    if (!tab && lane == 0) a.peers[p].Ab[row] = ab;
 }
 
-// k_p2p_wait: lane p waits for peer p's `per` workgroups of this step (kind 0 records, 1 rows)
+// k_p2p_wait: lane p waits for peer p's `per` signals of this step (kind 0 records, 1 rows):
+// relaxed system-scope polls (no cache invalidation per poll), one acquire fence at the end
 __device__ void p2p_wait(const StepArgs& a, int kind, unsigned per) {
     const int p = threadIdx.x;
     if (p >= a.G || p == a.rank) return;
@@ -129,13 +104,14 @@ __device__ void p2p_wait(const StepArgs& a, int kind, unsigned per) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     // a wait that already timed out this run: do not wait again (fail fast; rae_check raises)
     const bool dead = (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 64) != 0;
-    while (!dead && (int)(__hip_atomic_load(s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+    while (!dead && (int)(__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > RAE_P2P_TIMEOUT) {
             atomicOr(a.err, 64);
             break;
         }
         __builtin_amdgcn_s_sleep(2);
     }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);         // system scope: the peer's stores
     *ex = target;
 }
 
