@@ -439,7 +439,7 @@ def main():
         kern["k_forward"]["kernels"] = "k_bil_enc + k_bil_mt + k_bil_dec + k_bil_mt [+ k_bil_dp*] + k_bil_fin"
         kern["k_update"]["kernels"] = "[k_bil_prep +] k_bil_rows + k_update_bil"
     elif eng.kernel_forms_in_use()["sp_forward"] == "split":
-        kern["k_forward"]["kernels"] = "k_sp_enc + k_sp_cp + k_sp_dec + k_sp_ctdw + k_sp_fin"
+        kern["k_forward"]["kernels"] = "k_sp_enc + k_sp_cp + k_sp_dec + k_sp_ctdw (with the softmax backward)"
     # the roofline line names the dominant kernel: the longer average launch of the step
     dom = "k_forward" if fwd_us >= upd_us else "k_update"
     if dec == "sp":

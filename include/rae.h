@@ -98,7 +98,7 @@ typedef struct rae_config {
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
 #define RAE_SPFWD_FUSED 1     /* k_forward: one workgroup per example                         */
-#define RAE_SPFWD_SPLIT 2     /* k_sp_enc -> P.C^T GEMM -> k_sp_dec -> dw.C GEMM -> k_sp_fin    */
+#define RAE_SPFWD_SPLIT 2     /* k_sp_enc -> P.C^T GEMM -> k_sp_dec -> dw.C GEMM (+ dS epilogue)  */
 #define RAE_BILDP_AUTO 0      /* inside the second M-tile pass when bf16 and m <= 128          */
 #define RAE_BILDP_STRIDED 1   /* k_bil_dp (one wave per 16x16 tile of dP)                      */
 #define RAE_BILDP_STAGED 2    /* k_bil_dp2 (bf16, LDS-staged R slices; r <= 256, m <= 128)      */

@@ -76,10 +76,6 @@ __global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
     sp_split_ctdw<VEC>(a, blockIdx.x, red);
 }
-__global__ __launch_bounds__(RAE_BT) void k_sp_fin(StepArgs a) {
-    __shared__ float red[2 * RAE_NWAVE];
-    sp_split_fin(a, blockIdx.x, red);
-}
 // SP dense partials (data parallel): this rank's dC1 / dC2 / dWb into its records, before the exchange
 __global__ __launch_bounds__(RAE_BT) void k_dpart(StepArgs a) {
     __shared__ __attribute__((aligned(16))) rae_f4 sacc[RAE_BT];
@@ -951,7 +947,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     p->sp_split = !bil && (c.sp_forward == RAE_SPFWD_SPLIT ||
                            (c.sp_forward == RAE_SPFWD_AUTO &&
                             (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
-    const size_t o_dps = p->sp_split ? take(4ull * c.batch_size * c.relations) : 0;
+    const size_t o_dps = p->sp_split ? take(4ull * 2 * c.batch_size) : 0;   // (sd, sz) per example
     a.privnf = a.priv ? (a.dcap < 32 ? a.dcap : 32) : 0;
     a.privc = (a.priv && a.part && c.world_size > 1) ? 1 : 0;
     const size_t o_pmask = a.priv ? take(16ull * W_ * L) : 0;
@@ -1176,7 +1172,6 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         else RAE_LAUNCH(p, k_sp_dec<false>, gr, bt, p->smem_fwd, st, a);
         if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_BT), 0, st, a);
         else RAE_LAUNCH(p, k_sp_ctdw<false>, gct, dim3(RAE_BT), 0, st, a);
-        RAE_LAUNCH(p, k_sp_fin, gr, dim3(RAE_BT), 0, st, a);
         return;
     }
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;

@@ -7,10 +7,14 @@
 //   k_sp_enc   per example : S = X.W + Wb, P = softmax(S), H          -> record P; z, H parked
 //   k_sp_cp    GEMM        : V1 = P C1^T, V2 = P C2^T  (l x r, K = m)  -> record V1, V2
 //   k_sp_dec   per example : A rows, dots, scores, loss, coefficients, dw1, dw2, G1
-//   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r) -> workspace dPs
-//   k_sp_fin   per example : centred softmax backward                  -> record dS
+//   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r), and in its epilogue the
+//                            centred softmax backward, element-wise    -> record dS
+// The softmax backward's two sums per example come from k_sp_dec, not from a pass over dP:
+// sum_k P_k dP_k = <dw1, C1.P> + <dw2, C2.P> = <dw1, V1> + <dw2, V2> (V = k_sp_cp's vectors) and
+// sum_k P_k z_k -- so dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b)) needs nothing outside the
+// tile (round 5: the fifth launch, k_sp_fin, is gone; C4 forward 36 -> ~32 us).
 // Same arithmetic as sp_example (SelectionalPreferences.py:30-51, RelationClassifier.py:35-36,
-// OieModel.py:81); only the fp32 summation order of the two products differs.  Until k_sp_fin
+// OieModel.py:81); only the fp32 summation order of the two products differs.  Until k_sp_ctdw
 // the record's dS slot holds z = S - max S and, until k_sp_dec, its loss slot holds H.
 #pragma once
 #include "rae_sp.hpp"
@@ -251,10 +255,18 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     float o[4];
     sp_gemm_combine(acc, red, lane, w, o);
     if (w != 0) return;
+    // epilogue: dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b))   (softmax_backward's centred
+    // form; sd, sz per example from k_sp_dec)
+    const float ce = 2.f * a.alpha * a.invD;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][k = li]
         const int bo = bt * 16 + 4 * g + reg;
-        if (bo < l && kv) a.dPs[(int64_t)bo * m + k] = o[reg];
+        if (bo < l && kv) {
+            float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
+            const float pk = rec[a.lay.oP + k], zk = rec[a.lay.odS + k];
+            const float sd = a.dPs[2 * bo], sz = a.dPs[2 * bo + 1];
+            rec[a.lay.odS + k] = pk * ((o[reg] - sd) + ce * (zk - sz));
+        }
     }
 }
 
@@ -309,28 +321,19 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
         rec[a.lay.ocoef + 2 * j + 1] = c[2];
     }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
+    // the softmax backward's per-example sums for k_sp_ctdw's epilogue:
+    //   sd = sum_k P_k dP_k = <dw1, V1> + <dw2, V2>,  sz = sum_k P_k z_k  (z: the record's dS slot)
+    float x1 = 0.f, x2 = 0.f;
+    for (int i = threadIdx.x; i < r; i += RAE_FBT) x1 += S.sdw1[i] * S.swC1[i] + S.sdw2[i] * S.swC2[i];
+    for (int k = threadIdx.x; k < m; k += RAE_FBT) x2 += rec[a.lay.oP + k] * rec[a.lay.odS + k];
+    const float sd = block_sum<RAE_FBT>(x1, S.sred + 48);
+    const float sz = block_sum<RAE_FBT>(x2, S.sred + 56);
+    if (threadIdx.x == 0) {
+        a.dPs[2 * bl] = sd;
+        a.dPs[2 * bl + 1] = sz;
+    }
     RAE_STAMP(a, 6);
     RAE_STAMP(a, 7);
-}
-
-// k_sp_fin: dS_k = P_k((dP_k - sum P dP) + ce (z_k - sum P z)), as softmax_backward
-__device__ void sp_split_fin(const StepArgs& a, int bl, float* red) {
-    const int m = a.m;
-    float* rec = a.ex + (int64_t)(a.rank * a.l + bl) * a.lay.rec;
-    const float* dP = a.dPs + (int64_t)bl * m;
-    const float ce = 2.f * a.alpha * a.invD;
-    float sd = 0.f, sz = 0.f;
-    for (int k = threadIdx.x; k < m; k += RAE_BT) {
-        const float p = rec[a.lay.oP + k];
-        sd += p * dP[k];
-        sz += p * rec[a.lay.odS + k];
-    }
-    sd = block_sum<RAE_BT>(sd, red);
-    sz = block_sum<RAE_BT>(sz, red + RAE_NWAVE);
-    for (int k = threadIdx.x; k < m; k += RAE_BT) {
-        const float p = rec[a.lay.oP + k];
-        rec[a.lay.odS + k] = p * ((dP[k] - sd) + ce * (rec[a.lay.odS + k] - sz));
-    }
 }
 
 }  // namespace rae
