@@ -323,6 +323,9 @@ __device__ __forceinline__ void sp_project_back(const StepArgs& a, const D& Dm, 
 // barriers) for m <= 512: softmax, entropy.  Issues the A-row LDS-DMA and the decoder
 // register cache behind the W-row loads.  Leaves H (alpha-scaled) in S.sred[40] and the
 // shifted scores z = S - max(S) in S.sZ (log P = z - lse; see softmax_backward).
+#ifndef RAE_ENC_KF
+#define RAE_ENC_KF 4
+#endif
 template <bool V4, bool V4R, bool LOADC, class D, class Cache>
 __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, ExampleSmem& S,
                                                 int NR, int skip_e2, Cache& cc_,
@@ -348,9 +351,24 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         __syncthreads();
         if (!issued) gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
         if (slot < nslot) {
+            // RAE_ENC_KF rows' loads in flight per round (the feature order of the sum is kept):
+            // W is a random-row gather from HBM, and one dependent load per feature had put
+            // nf / nslot full round trips on the chain (C4: m = 300, 6 slots, ~14 features)
             for (int cc = c; cc < mv; cc += RAE_FBT)          // mv > RAE_FBT only for huge m
-                for (int f = slot; f < nf; f += nslot)
-                    vfma(acc, S.sfval[f], Wv[(int64_t)S.sfidx[f] * mv + cc]);
+                for (int f0 = slot; f0 < nf; f0 += nslot * RAE_ENC_KF) {
+                    VT wv[RAE_ENC_KF];
+                    float fv[RAE_ENC_KF];
+#pragma unroll
+                    for (int u = 0; u < RAE_ENC_KF; ++u) {
+                        const int f = f0 + u * nslot;
+                        const bool ok = f < nf;
+                        wv[u] = Wv[(int64_t)S.sfidx[ok ? f : f0] * mv + cc];
+                        fv[u] = ok ? S.sfval[f] : 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < RAE_ENC_KF; ++u)
+                        if (f0 + u * nslot < nf) vfma(acc, fv[u], wv[u]);
+                }
         }
         if (LOADC && !issued) cc_.load(a, Dm, 0, 0);         // behind the W-row loads
         issued = true;
