@@ -227,6 +227,20 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const bool bv = b < l, kv = k < m;
     const float* dwr = a.dwb + (int64_t)(a.rank * l + (bv ? b : 0)) * a.dws;
     const int kc = kv ? k : 0;
+    // the epilogue's operands (wave 0): P, z and the example's two sums of its four output rows,
+    // loaded before the GEMM so they are not a dependent round trip after it
+    float pk[4], zk[4], sd[4], sz[4];
+    if (w == 0) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int bo = min(bt * 16 + 4 * g + reg, l - 1);
+            const float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
+            pk[reg] = rec[a.lay.oP + kc];
+            zk[reg] = rec[a.lay.odS + kc];
+            sd[reg] = a.dPs[2 * bo];
+            sz[reg] = a.dPs[2 * bo + 1];
+        }
+    }
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int nci = (r + 15) / 16, nch = 2 * nci;
     for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
@@ -263,9 +277,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
         const int bo = bt * 16 + 4 * g + reg;
         if (bo < l && kv) {
             float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
-            const float pk = rec[a.lay.oP + k], zk = rec[a.lay.odS + k];
-            const float sd = a.dPs[2 * bo], sz = a.dPs[2 * bo + 1];
-            rec[a.lay.odS + k] = pk * ((o[reg] - sd) + ce * (zk - sz));
+            rec[a.lay.odS + k] = pk[reg] * ((o[reg] - sd[reg]) + ce * (zk[reg] - sz[reg]));
         }
     }
 }
