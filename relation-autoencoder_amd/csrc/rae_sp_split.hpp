@@ -9,7 +9,7 @@
 //   k_sp_dec   per example : A rows, dots, scores, loss, coefficients, dw1, dw2, G1
 //   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r), and in its epilogue the
 //                            centred softmax backward, element-wise    -> record dS
-// The softmax backward's two sums per example come from k_sp_dec, not from a pass over dP:
+// The softmax backward's two sums per example come from k_sp_enc / k_sp_dec, not from dP:
 // sum_k P_k dP_k = <dw1, C1.P> + <dw2, C2.P> = <dw1, V1> + <dw2, V2> (V = k_sp_cp's vectors) and
 // sum_k P_k z_k -- so dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b)) needs nothing outside the
 // tile (round 5: the fifth launch, k_sp_fin, is gone; C4 forward 36 -> ~32 us).
@@ -40,6 +40,12 @@ __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
         rec[a.lay.odS + k] = S.sZ[k];
     }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];
+    if (threadIdx.x < RAE_WAVE) {                // sz = sum_k P_k z_k for k_sp_ctdw's epilogue
+        float x = 0.f;
+        for (int k = threadIdx.x; k < m; k += RAE_WAVE) x += S.sP[k] * S.sZ[k];
+        x = wave_sum(x);
+        if (threadIdx.x == 0) a.dPs[2 * bl + 1] = x;
+    }
 }
 
 // four fp32 MFMAs over a 16-deep K chunk: lane (li, g) supplies K = k0 + 4g + j for MFMA j
@@ -333,17 +339,12 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
         rec[a.lay.ocoef + 2 * j + 1] = c[2];
     }
     if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
-    // the softmax backward's per-example sums for k_sp_ctdw's epilogue:
-    //   sd = sum_k P_k dP_k = <dw1, V1> + <dw2, V2>,  sz = sum_k P_k z_k  (z: the record's dS slot)
-    float x1 = 0.f, x2 = 0.f;
+    // the softmax backward's sum for k_sp_ctdw's epilogue: sd = sum_k P_k dP_k
+    // = <dw1, V1> + <dw2, V2> (k_sp_enc left sz = sum_k P_k z_k)
+    float x1 = 0.f;
     for (int i = threadIdx.x; i < r; i += RAE_FBT) x1 += S.sdw1[i] * S.swC1[i] + S.sdw2[i] * S.swC2[i];
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) x2 += rec[a.lay.oP + k] * rec[a.lay.odS + k];
     const float sd = block_sum<RAE_FBT>(x1, S.sred + 48);
-    const float sz = block_sum<RAE_FBT>(x2, S.sred + 56);
-    if (threadIdx.x == 0) {
-        a.dPs[2 * bl] = sd;
-        a.dPs[2 * bl + 1] = sz;
-    }
+    if (threadIdx.x == 0) a.dPs[2 * bl] = sd;
     RAE_STAMP(a, 6);
     RAE_STAMP(a, 7);
 }
