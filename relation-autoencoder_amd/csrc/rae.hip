@@ -69,11 +69,11 @@ __global__ __launch_bounds__(RAE_BT) void k_sp_cp(StepArgs a) {
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_sp_dec(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    sp_split_dec<V4>(a, step_batch(a), blockIdx.x, smem);
+    sp_split_dec<V4>(a, step_batch(a), blockIdx.x >> 1, blockIdx.x & 1, smem);   // (example, side)
 }
 template <bool VEC>
 __global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
-    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4];
+    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4 + 16];
     sp_split_ctdw<VEC>(a, blockIdx.x, red);
 }
 // SP dense partials (data parallel): this rank's dC1 / dC2 / dWb into its records, before the exchange
@@ -620,6 +620,7 @@ struct rae_plan {
     bool mt_direct = false; // fp32 blocks beyond LDS (m > 320): k_bil_mt reads R from L2
     bool sp_split = false;  // SP forward as enc -> GEMM -> dec -> GEMM -> fin (large shapes)
     size_t smem_spe = 0;    // k_sp_enc
+    size_t smem_spd = 0;    // k_sp_dec (one negative side)
     bool mt_bf16 = false;
     int grid_fwd = 0, grid_update = 0, grid_dense = 0;
     bool v4 = false;
@@ -947,7 +948,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     p->sp_split = !bil && (c.sp_forward == RAE_SPFWD_SPLIT ||
                            (c.sp_forward == RAE_SPFWD_AUTO &&
                             (int64_t)c.embed * c.relations > RAE_SPLIT_RM));
-    const size_t o_dps = p->sp_split ? take(4ull * 2 * c.batch_size) : 0;   // (sd, sz) per example
+    const size_t o_sps = p->sp_split ? take(4ull * sps_stride(c.embed) * c.batch_size) : 0;
     a.privnf = a.priv ? (a.dcap < 32 ? a.dcap : 32) : 0;
     a.privc = (a.priv && a.part && c.world_size > 1) ? 1 : 0;
     const size_t o_pmask = a.priv ? take(16ull * W_ * L) : 0;
@@ -1002,7 +1003,8 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.regpart = reinterpret_cast<double*>(p->ws + o_reg);
     a.gWs = a.reg_on ? reinterpret_cast<float*>(p->ws + o_gws) : nullptr;
     a.dPpart = bil ? reinterpret_cast<float*>(p->ws + o_dpp) : nullptr;
-    a.dPs = p->sp_split ? reinterpret_cast<float*>(p->ws + o_dps) : nullptr;
+    a.sps = p->sp_split ? reinterpret_cast<float*>(p->ws + o_sps) : nullptr;
+    a.spss = sps_stride(c.embed);
     a.mtV = bil ? reinterpret_cast<float*>(p->ws + o_mtv) : nullptr;
     a.mtW = bil ? reinterpret_cast<float*>(p->ws + o_mtw) : nullptr;
     a.mtP = mtdp ? reinterpret_cast<float*>(p->ws + o_mtp) : nullptr;
@@ -1027,6 +1029,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     p->smem_idxf = 8ull * RAE_IDX_FAST + 4ull * 64 + 4ull * RAE_IDX_FAST;
     p->smem_fwd = smem_ex;
     p->smem_spe = p->sp_split ? 4ull * example_smem_floats(0, c.relations, c.embed, 0) : 0;
+    p->smem_spd = p->sp_split ? 4ull * sp_dec_side_smem_floats(c.embed, c.neg_samples) : 0;
     p->smem_dec = bil ? 4ull * bil_dec_smem_floats(c.embed, c.neg_samples) : 0;
     // the M-tile passes: bf16 blocks need m <= 128 (four K steps of 32 per fragment set)
     p->mt_bf16 = bil && a.bf16 && c.relations <= 128;
@@ -1168,8 +1171,9 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         else RAE_LAUNCH(p, k_sp_enc<false>, gr, bt, p->smem_spe, st, a);
         if (a.m % 4 == 0) RAE_LAUNCH(p, k_sp_cp<true>, gcp, dim3(RAE_BT), 0, st, a);
         else RAE_LAUNCH(p, k_sp_cp<false>, gcp, dim3(RAE_BT), 0, st, a);
-        if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gr, bt, p->smem_fwd, st, a);
-        else RAE_LAUNCH(p, k_sp_dec<false>, gr, bt, p->smem_fwd, st, a);
+        const dim3 gsd(2 * p->grid_fwd);                   // two workgroups (sides) per example
+        if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gsd, bt, p->smem_spd, st, a);
+        else RAE_LAUNCH(p, k_sp_dec<false>, gsd, bt, p->smem_spd, st, a);
         if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_BT), 0, st, a);
         else RAE_LAUNCH(p, k_sp_ctdw<false>, gct, dim3(RAE_BT), 0, st, a);
         return;

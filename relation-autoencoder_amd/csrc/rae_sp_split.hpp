@@ -6,22 +6,53 @@
 // batch as fp32-MFMA GEMMs, and the per-example work is split around them:
 //   k_sp_enc   per example : S = X.W + Wb, P = softmax(S), H          -> record P; z, H parked
 //   k_sp_cp    GEMM        : V1 = P C1^T, V2 = P C2^T  (l x r, K = m)  -> record V1, V2
-//   k_sp_dec   per example : A rows, dots, scores, loss, coefficients, dw1, dw2, G1
-//   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r), and in its epilogue the
-//                            centred softmax backward, element-wise    -> record dS
+//   k_sp_dec   two workgroups per example, one per negative side (h = 0: neg1, 1: neg2): A[e1]
+//              and that side's s rows, dots, the side's coefficients and its weighted row sum
+//              N_h = sum_t dg_t A[neg_h,t]  -> scratch (N_h, A[e1], per-example scalars)
+//   k_sp_ctdw  GEMM        : dP = dw1 C1 + dw2 C2      (l x m, K = 2r), the operand assembled as it
+//                            loads (dw1 = dl A[e1] + N1, dw2 = dr A[e1] + N2: dl, dr need both
+//                            sides' sums), and in its epilogue the centred softmax backward,
+//                            element-wise -> record dS; the tiles also store dw1, dw2, G1 (or dl,
+//                            dr for the wire record) and the loss
 // The softmax backward's two sums per example come from k_sp_enc / k_sp_dec, not from dP:
-// sum_k P_k dP_k = <dw1, C1.P> + <dw2, C2.P> = <dw1, V1> + <dw2, V2> (V = k_sp_cp's vectors) and
-// sum_k P_k z_k -- so dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b)) needs nothing outside the
-// tile (round 5: the fifth launch, k_sp_fin, is gone; C4 forward 36 -> ~32 us).
+// sum_k P_k dP_k = <dw1, C1.P> + <dw2, C2.P> = dl left + <N1, V1> + dr right + <N2, V2> (V = k_sp_cp's
+// vectors, left / right = <V1, A[e1]>, <V2, A[e1]>) and sum_k P_k z_k -- so
+// dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b)) needs nothing outside the tile (round 5: the
+// fifth launch, k_sp_fin, is gone, and the decoder's 121 KB A-row gather per example at C4 is
+// split over two workgroups).
 // Same arithmetic as sp_example (SelectionalPreferences.py:30-51, RelationClassifier.py:35-36,
-// OieModel.py:81); only the fp32 summation order of the two products differs.  Until k_sp_ctdw
-// the record's dS slot holds z = S - max S and, until k_sp_dec, its loss slot holds H.
+// OieModel.py:81); only the fp32 summation order of the products and row sums differs.  Until
+// k_sp_ctdw the record's dS slot holds z = S - max S and its loss slot holds H.
 #pragma once
 #include "rae_sp.hpp"
 
 namespace rae {
 
 typedef float rae_f32x4 __attribute__((ext_vector_type(4)));
+
+// per-example scratch of the split forward (a.sps, stride a.spss = sps_stride(r)):
+// [N1 (r4) | N2 (r4) | A[e1] (r4) | scalars (16)]
+enum {
+    SPS_SZ = 0,      // sum_k P_k z_k (k_sp_enc)
+    SPS_LEFT,        // <V1, A[e1]>, <V2, A[e1]>      (k_sp_dec, side 0)
+    SPS_RIGHT,
+    SPS_DU1,         // d cost / d u1, u2 (positive scores)
+    SPS_DU2,
+    SPS_LBASE,       // -softplus(-u1) - softplus(-u2) + 2 H
+    SPS_SDG1,        // side 0: sum of its coefficients, sum of its log sigmoids, <N1, V1>
+    SPS_SLS1,
+    SPS_NV1,
+    SPS_SDG2,        // side 1: the same for neg2 and V2
+    SPS_SLS2,
+    SPS_NV2
+};
+__host__ __device__ inline int sps_stride(int r) { return 3 * align4(r) + 16; }
+// LDS of one k_sp_dec side: V1, V2, the 1 + s rows, dots / ids / Ab / coefficients, the row-sum
+// partials (<= 8 groups) and the block-sum scratch
+__host__ __device__ inline int sp_dec_side_smem_floats(int r, int s) {
+    const int r4 = align4(r), s4 = align4(s + 2);
+    return 2 * r4 + (1 + s) * r4 + 4 * s4 + 8 * r4 + 64;
+}
 
 template <bool V4>
 __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
@@ -44,7 +75,7 @@ __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
         float x = 0.f;
         for (int k = threadIdx.x; k < m; k += RAE_WAVE) x += S.sP[k] * S.sZ[k];
         x = wave_sum(x);
-        if (threadIdx.x == 0) a.dPs[2 * bl + 1] = x;
+        if (threadIdx.x == 0) a.sps[(int64_t)bl * a.spss + 3 * align4(Dm.r) + SPS_SZ] = x;
     }
 }
 
@@ -220,22 +251,52 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     }
 }
 
-// k_sp_ctdw: tile (example, k) of dP.  A = dw (rows b, K = i: one float4 per lane per chunk),
-// B = C (K = i rows, columns k: four strided scalars per lane); K runs over C1's then C2's i.
+// k_sp_ctdw: tile (example, k) of dP.  A = dw (rows b, K = i: one float4 per lane per chunk,
+// assembled as it loads: dl A[e1] + N1 / dr A[e1] + N2), B = C (K = i rows, columns k: four
+// strided scalars per lane); K runs over C1's then C2's i.  Besides dS the tile stores, for its
+// 16 examples and the embedding columns i = 16 kt + (0..15) (+ 16 nkt q), dw1, dw2 (what the
+// update's dense tiles read) and G1 = dl V1 + dr V2 (or dl, dr for the wire record), and tile
+// kt = 0 the loss -- their loads issued before the GEMM, their stores after it.
 template <bool VEC>
 __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
-    const int l = a.l, m = a.m, r = a.r;
+    const int l = a.l, m = a.m, r = a.r, r4 = align4(r);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nkt = (m + 15) / 16;
     const int bt = task / nkt, kt = task - bt * nkt;
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, k = kt * 16 + li;
     const bool bv = b < l, kv = k < m;
-    const float* dwr = a.dwb + (int64_t)(a.rank * l + (bv ? b : 0)) * a.dws;
+    float* sdl = red + RAE_BT * 4;                        // [16]: sd of the tile's examples
+    // this lane's GEMM row (example b): dl, dr from both sides' sums
+    const float* spb = a.sps + (int64_t)(bv ? b : 0) * a.spss;
+    const float* scb = spb + 3 * r4;
+    const float du1b = scb[SPS_DU1], du2b = scb[SPS_DU2];
+    const float dlb = du1b + du2b + scb[SPS_SDG2];      // as sp_coefficients: d cost / d left
+    const float drb = du1b + du2b + scb[SPS_SDG1];
+    float lft = 0.f, rgt = 0.f, nv1 = 0.f, nv2 = 0.f;
+    if (w == 0 && g == 0) {
+        lft = scb[SPS_LEFT]; rgt = scb[SPS_RIGHT]; nv1 = scb[SPS_NV1]; nv2 = scb[SPS_NV2];
+    }
+    // the tile's stores of dw1, dw2, G1: pair (example eo, column ii) per thread
+    const int pr = threadIdx.x, eo = pr >> 4, ii = pr & 15;
+    const int bo_s = bt * 16 + eo;
+    const bool sv = bo_s < l;
+    const int bs = sv ? bo_s : 0;
+    const float* sps_s = a.sps + (int64_t)bs * a.spss;
+    const int is0 = kt * 16 + ii;
+    const bool iv0 = sv && is0 < r;
+    const int ic0 = iv0 ? is0 : 0;
+    const float s_du1 = sps_s[3 * r4 + SPS_DU1], s_du2 = sps_s[3 * r4 + SPS_DU2];
+    const float s_sdg1 = sps_s[3 * r4 + SPS_SDG1], s_sdg2 = sps_s[3 * r4 + SPS_SDG2];
+    const float* vrow = a.vb + (int64_t)(a.rank * l + bs) * a.vbs;
+    const float sa0 = sps_s[2 * r4 + ic0], sn10 = sps_s[ic0], sn20 = sps_s[r4 + ic0];
+    const float sv10 = vrow[a.vV1 + ic0], sv20 = vrow[a.vV2 + ic0];
+    const bool lossl = kt == 0 && ii == 0 && sv;
+    const float lbase = lossl ? sps_s[3 * r4 + SPS_LBASE] : 0.f;
+    const float sls = lossl ? sps_s[3 * r4 + SPS_SLS1] + sps_s[3 * r4 + SPS_SLS2] : 0.f;
+    // the epilogue's operands (wave 0): P, z and sz of its four output rows
     const int kc = kv ? k : 0;
-    // the epilogue's operands (wave 0): P, z and the example's two sums of its four output rows,
-    // loaded before the GEMM so they are not a dependent round trip after it
-    float pk[4], zk[4], sd[4], sz[4];
+    float pk[4], zk[4], sz[4];
     if (w == 0) {
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
@@ -243,8 +304,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             const float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
             pk[reg] = rec[a.lay.oP + kc];
             zk[reg] = rec[a.lay.odS + kc];
-            sd[reg] = a.dPs[2 * bo];
-            sz[reg] = a.dPs[2 * bo + 1];
+            sz[reg] = a.sps[(int64_t)bo * a.spss + 3 * r4 + SPS_SZ];
         }
     }
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -256,9 +316,12 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             const int c = c0 + u * RAE_NWAVE;
             const bool cv = c < nch;
             const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
-            const float* Dw = dwr + (which ? a.dw2o : a.dw1o);
             const float* Cm = which ? a.C2 : a.C1;
-            x[u] = load4_guard<VEC>(Dw, i, r, bv && cv);
+            const float4 nn = load4_guard<VEC>(spb + which * r4, i, r, bv && cv);
+            const float4 ae = load4_guard<VEC>(spb + 2 * r4, i, r, bv && cv);
+            const float dd = which ? drb : dlb;
+            x[u] = make_float4(fmaf(dd, ae.x, nn.x), fmaf(dd, ae.y, nn.y),
+                               fmaf(dd, ae.z, nn.z), fmaf(dd, ae.w, nn.w));
             // branch-free strided column loads (clamped row, select after)
             const bool o0 = cv && kv && i < r, o1 = cv && kv && i + 1 < r;
             const bool o2 = cv && kv && i + 2 < r, o3 = cv && kv && i + 3 < r;
@@ -272,79 +335,194 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
 #pragma unroll
         for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
     }
+    // dw1, dw2 and G1 (the same fmaf forms as the GEMM operand and as k_vrec)
+    {
+        const float dl = s_du1 + s_du2 + s_sdg2, dr = s_du1 + s_du2 + s_sdg1;
+        float* dwr = a.dwb + (int64_t)(a.rank * l + bs) * a.dws;
+        float* rec = a.ex + (int64_t)(a.rank * l + bs) * a.lay.rec;
+        if (iv0) {
+            dwr[a.dw1o + is0] = fmaf(dl, sa0, sn10);
+            dwr[a.dw2o + is0] = fmaf(dr, sa0, sn20);
+            if (!a.lay.wire) rec[a.lay.oG1 + is0] = fmaf(dl, sv10, dr * sv20);
+        }
+        for (int is = is0 + 16 * nkt; sv && is < r; is += 16 * nkt) {    // r > 16 nkt only
+            const float ae = sps_s[2 * r4 + is];
+            dwr[a.dw1o + is] = fmaf(dl, ae, sps_s[is]);
+            dwr[a.dw2o + is] = fmaf(dr, ae, sps_s[r4 + is]);
+            if (!a.lay.wire) rec[a.lay.oG1 + is] = fmaf(dl, vrow[a.vV1 + is], dr * vrow[a.vV2 + is]);
+        }
+        if (lossl) {
+            rec[a.lay.oloss] = lbase + sls;
+            if (a.lay.wire) {                             // k_vrec rebuilds G1 from (dl, dr)
+                rec[a.lay.oAux + 0] = dl;
+                rec[a.lay.oAux + 1] = dr;
+            }
+        }
+    }
+    if (w == 0 && g == 0) sdl[li] = fmaf(dlb, lft, nv1) + fmaf(drb, rgt, nv2);
     float o[4];
-    sp_gemm_combine(acc, red, lane, w, o);
+    sp_gemm_combine(acc, red, lane, w, o);                // its barrier also publishes sdl
     if (w != 0) return;
     // epilogue: dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b))   (softmax_backward's centred
-    // form; sd, sz per example from k_sp_dec)
+    // form)
     const float ce = 2.f * a.alpha * a.invD;
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {                   // D[b = 4g + reg][k = li]
         const int bo = bt * 16 + 4 * g + reg;
         if (bo < l && kv) {
             float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
-            rec[a.lay.odS + k] = pk[reg] * ((o[reg] - sd[reg]) + ce * (zk[reg] - sz[reg]));
+            rec[a.lay.odS + k] = pk[reg] * ((o[reg] - sdl[4 * g + reg]) + ce * (zk[reg] - sz[reg]));
         }
     }
 }
 
+// k_sp_dec, one side h of example bl: the A rows of e1 and of the side's s negatives by LDS-DMA
+// (half the example's gather), the dots <V1, A[e1]>, <V2, A[e1]> and <V_h, A[neg_h,t]>, the side's
+// coefficients (its record entries written here), its weighted row sum N_h and <N_h, V_h>; side
+// 0 also the positive scores' terms and a copy of A[e1].  The assembly dw = d A[e1] + N waits
+// for both sides: k_sp_ctdw.
 template <bool V4>
-__device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, char* smem) {
-    const DynDims Dm(a);
-    const int m = Dm.m, r = Dm.r, s = Dm.s, NR = 1 + 2 * s, NJ = 2 + 2 * s;
-    ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
+__device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* smem) {
+    typedef typename VecT<V4>::T VT;
+    constexpr int VW = V4 ? 4 : 1;
+    const int r = a.r, s = a.s, r4 = align4(r), rv = r / VW, r4v = r4 / VW, s4 = align4(s + 2);
+    const int NR = 1 + s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float* p = reinterpret_cast<float*>(smem);
+    float* sV1 = p; p += r4;
+    float* sV2 = p; p += r4;
+    float* srows = p; p += NR * r4;
+    float* sdots = p; p += s4;            // [0] left, [1] right, [2 + t] negative t
+    float* sAb = p; p += s4;              // [0] e1, [1] e2, [2 + t] negative t
+    float* scf = p; p += s4;              // coefficient of negative t
+    int* sid = reinterpret_cast<int*>(p); p += s4;
+    float* spart = p; p += 8 * r4;
+    float* sred = p;
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    float* sp = a.sps + (int64_t)bl * a.spss;
+    float* scl = sp + 3 * r4;
     RAE_STAMP(a, 0);
-    load_ids(a, Dm, ex, col, S);
-    const float H = rec[a.lay.oloss];
+    if (threadIdx.x < s + 2) {
+        const int j = threadIdx.x;
+        const int* src = j == 0 ? a.args1 + ex : j == 1 ? a.args2 + ex
+                       : (h ? a.neg2 : a.neg1) + (int64_t)(j - 2) * a.neg_stride + col;
+        sid[j] = *src;
+    }
+    const float H = (h == 0 && threadIdx.x == 0) ? rec[a.lay.oloss] : 0.f;
     __syncthreads();
     RAE_STAMP(a, 1);
-    if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
-    gather_rows_dma<V4>(a, Dm, S, NR, 1);
+    if (threadIdx.x < s + 2) sAb[threadIdx.x] = a.Ab[sid[threadIdx.x]];
+    {   // rho 0: A[e1]; rho >= 1: negative rho - 1 (id slot rho + 1)
+        const int nchunk = (rv + 63) / 64;
+        for (int t = w; t < NR * nchunk; t += RAE_FNW) {
+            const int rho = t / nchunk, ch = t - rho * nchunk;
+            const int c = ch * 64 + lane;
+            float* dst = srows + rho * r4 + ch * 64 * VW;
+            if (c < rv) {
+                const float* src = a.A + (int64_t)sid[rho ? rho + 1 : 0] * r + (int64_t)c * VW;
+                if constexpr (V4)
+                    __builtin_amdgcn_global_load_lds((rae_glob_void*)src, (rae_lds_void*)dst, 16, 0, 0);
+                else
+                    __builtin_amdgcn_global_load_lds((rae_glob_void*)src, (rae_lds_void*)dst, 4, 0, 0);
+            }
+        }
+    }
     const float* vrow = a.vb + (int64_t)bg * a.vbs;          // k_sp_cp's V1, V2
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        S.swC1[i] = vrow[a.vV1 + i];
-        S.swC2[i] = vrow[a.vV2 + i];
+        sV1[i] = vrow[a.vV1 + i];
+        sV2[i] = vrow[a.vV2 + i];
     }
-    __syncthreads();                                      // the A-row DMA has landed
+    __syncthreads();                                          // the A-row DMA has landed
     RAE_STAMP(a, 2);
-    sp_dots<V4>(Dm, S);
+    {   // dots, 16 lanes each (sp_dots' arithmetic): t = 0 left, 1 right, 2 + u negative u
+        const VT* Rv = reinterpret_cast<const VT*>(srows);
+        const VT* W1 = reinterpret_cast<const VT*>(sV1);
+        const VT* W2 = reinterpret_cast<const VT*>(sV2);
+        const VT* Wh = h ? W2 : W1;
+        const int ndot = s + 2;
+        for (int base = 0; base < ndot * 16; base += RAE_FBT) {
+            const int idx = base + threadIdx.x, t = idx >> 4, q = idx & 15;
+            float d = 0.f;
+            if (t < ndot) {
+                const VT* wv = t == 0 ? W1 : (t == 1 ? W2 : Wh);
+                const VT* x = Rv + (t < 2 ? 0 : t - 1) * r4v;
+                for (int c = q; c < rv; c += 16) d += vdot(x[c], wv[c]);
+            }
+            d = group16_sum(d);
+            if (t < ndot && q == 0) sdots[t] = d;
+        }
+    }
     __syncthreads();
     RAE_STAMP(a, 3);
-    sp_coefficients(a, Dm, S, H);
+    if (w == 0) {   // the side's coefficients (sp_coefficients' arithmetic), one wave
+        const float left = sdots[0], right = sdots[1], oth = h ? left : right;
+        float sdg = 0.f, sls = 0.f;
+        for (int t = lane; t < s; t += RAE_WAVE) {
+            const float gg = sdots[2 + t] + oth + sAb[2 + t];
+            float sg, spl;
+            sigmoid_softplus(gg, sg, spl);
+            const float dg = sg * a.invD;
+            scf[t] = dg;
+            const int j = 2 + h * s + t;
+            rec[a.lay.ocoef + 2 * j] = dg;
+            rec[a.lay.ocoef + 2 * j + 1] = dg;
+            sdg += dg;
+            sls -= spl;                                       // log sigmoid(-g) = -softplus(g)
+        }
+        sdg = wave_sum(sdg);
+        sls = wave_sum(sls);
+        if (lane == 0) {
+            scl[h ? SPS_SDG2 : SPS_SDG1] = sdg;
+            scl[h ? SPS_SLS2 : SPS_SLS1] = sls;
+            if (h == 0) {
+                const float one = left + right;
+                const float u1 = one + sAb[0], u2 = one + sAb[1];
+                float su1, pu1, su2, pu2;                     // sigmoid(-u), softplus(-u)
+                sigmoid_softplus(-u1, su1, pu1);
+                sigmoid_softplus(-u2, su2, pu2);
+                const float du1 = -su1 * a.invD, du2 = -su2 * a.invD;
+                scl[SPS_LEFT] = left;
+                scl[SPS_RIGHT] = right;
+                scl[SPS_DU1] = du1;
+                scl[SPS_DU2] = du2;
+                scl[SPS_LBASE] = -pu1 - pu2 + 2.f * H;        // log sigmoid(u) = -softplus(-u)
+                rec[a.lay.ocoef + 0] = 1.f;                   // e1: left / right carry it
+                rec[a.lay.ocoef + 1] = du1;
+                rec[a.lay.ocoef + 2] = 0.f;
+                rec[a.lay.ocoef + 3] = du2;
+            }
+        }
+    }
     __syncthreads();
     RAE_STAMP(a, 4);
-    sp_weighted_rows<V4>(Dm, S);
+    // N_h = sum_t dg_t A[neg_h,t]: thread owns (vector column, row group), groups in fixed order
+    const int ngrp = RAE_FBT / rv > 8 ? 8 : (RAE_FBT / rv > 0 ? RAE_FBT / rv : 1);
+    {
+        const int grp = threadIdx.x / rv, c = threadIdx.x - grp * rv;
+        if (grp < ngrp && rv <= RAE_FBT) {
+            const VT* R = reinterpret_cast<const VT*>(srows);
+            VT v;
+            vzero(v);
+            for (int t = grp; t < s; t += ngrp) vfma(v, scf[t], R[(1 + t) * r4v + c]);
+            reinterpret_cast<VT*>(spart)[grp * rv + c] = v;
+        }
+    }
     __syncthreads();
     RAE_STAMP(a, 5);
-    const float dl = S.scoef[0], dr = S.scoef[1];
-    float* dwr = a.dwb + (int64_t)bg * a.dws;
-    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
-        dwr[a.dw1o + i] = S.sdw1[i];
-        dwr[a.dw2o + i] = S.sdw2[i];
-        // A[e1]'s vector, one explicit fma (k_vrec forms it the same way: bit-identical)
-        if (!a.lay.wire) rec[a.lay.oG1 + i] = fmaf(dl, S.swC1[i], dr * S.swC2[i]);
-    }
-    if (a.lay.wire && threadIdx.x == 0) {                 // k_vrec rebuilds G1 from (dl, dr)
-        rec[a.lay.oAux + 0] = dl;
-        rec[a.lay.oAux + 1] = dr;
-    }
-    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
-        const float* c = S.scoef + 3 * j;
-        const float cj = j == 0 ? 1.f : (j == 1 ? 0.f : (j < 2 + s ? c[0] : c[1]));
-        rec[a.lay.ocoef + 2 * j] = cj;
-        rec[a.lay.ocoef + 2 * j + 1] = c[2];
-    }
-    if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
-    // the softmax backward's sum for k_sp_ctdw's epilogue: sd = sum_k P_k dP_k
-    // = <dw1, V1> + <dw2, V2> (k_sp_enc left sz = sum_k P_k z_k)
+    const float* sVh = h ? sV2 : sV1;
     float x1 = 0.f;
-    for (int i = threadIdx.x; i < r; i += RAE_FBT) x1 += S.sdw1[i] * S.swC1[i] + S.sdw2[i] * S.swC2[i];
-    const float sd = block_sum<RAE_FBT>(x1, S.sred + 48);
-    if (threadIdx.x == 0) a.dPs[2 * bl] = sd;
+    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
+        float v = 0.f;
+        for (int gg = 0; gg < ngrp; ++gg) v += spart[gg * r + i];
+        sp[h * r4 + i] = v;
+        x1 += v * sVh[i];
+        if (h == 0) sp[2 * r4 + i] = srows[i];                // A[e1] for the assembly
+    }
+    const float nv = block_sum<RAE_FBT>(x1, sred);
+    if (threadIdx.x == 0) scl[h ? SPS_NV2 : SPS_NV1] = nv;
     RAE_STAMP(a, 6);
     RAE_STAMP(a, 7);
 }

@@ -178,7 +178,8 @@ struct StepArgs {
     float* costs;
     float* gWs;          // dense W gradient scratch (reg_on only)
     float* dPpart;       // bilinear: dCost/dP partial sums over i-blocks (nib, l, m)
-    float* dPs;          // split SP forward (rae_sp_split.hpp): dP = dw1 C1 + dw2 C2 (l, m)
+    float* sps;          // split SP forward (rae_sp_split.hpp): per example of the rank, the
+    int spss;            //   decoder halves' N1 | N2 | A[e1] rows and their scalars (stride spss)
     float* mtV;          // bilinear: k_bil_mt partials over j-blocks (nblk, l, r4): M a2 / M y
     float* mtW;          //           ... over i-blocks: M^T a1 / M^T x
     float* mtP;          //           dP partials of the second pass, per block (nmtp, l, m)
