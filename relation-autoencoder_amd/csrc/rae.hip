@@ -69,7 +69,7 @@ __global__ __launch_bounds__(RAE_BT) void k_sp_cp(StepArgs a) {
 template <bool V4>
 __global__ __launch_bounds__(RAE_FBT) void k_sp_dec(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    sp_split_dec<V4>(a, step_batch(a), blockIdx.x >> 1, blockIdx.x & 1, smem);   // (example, side)
+    sp_split_dec<V4>(a, step_batch(a), blockIdx.x / RAE_SPD_NP, blockIdx.x % RAE_SPD_NP, smem);
 }
 template <bool VEC>
 __global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
@@ -1171,7 +1171,7 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         else RAE_LAUNCH(p, k_sp_enc<false>, gr, bt, p->smem_spe, st, a);
         if (a.m % 4 == 0) RAE_LAUNCH(p, k_sp_cp<true>, gcp, dim3(RAE_BT), 0, st, a);
         else RAE_LAUNCH(p, k_sp_cp<false>, gcp, dim3(RAE_BT), 0, st, a);
-        const dim3 gsd(2 * p->grid_fwd);                   // two workgroups (sides) per example
+        const dim3 gsd(RAE_SPD_NP * p->grid_fwd);          // a workgroup per (example, piece)
         if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gsd, bt, p->smem_spd, st, a);
         else RAE_LAUNCH(p, k_sp_dec<false>, gsd, bt, p->smem_spd, st, a);
         if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_BT), 0, st, a);

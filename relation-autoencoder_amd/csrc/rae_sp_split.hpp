@@ -30,28 +30,33 @@ namespace rae {
 
 typedef float rae_f32x4 __attribute__((ext_vector_type(4)));
 
+// k_sp_dec pieces: each negative side is split into RAE_SPD_NQ ranges of negatives, one
+// workgroup each (2 RAE_SPD_NQ workgroups per example)
+#ifndef RAE_SPD_NQ
+#define RAE_SPD_NQ 1   // measured (C4 forward, events): 1 -> 28.6 us, 2 -> 30.8, 3 -> 38.0
+#endif
+#define RAE_SPD_NP (2 * RAE_SPD_NQ)
+static_assert(RAE_SPD_NQ >= 1 && 8 + 3 * RAE_SPD_NP <= 32, "pieces' scalars fit the 32-float block");
 // per-example scratch of the split forward (a.sps, stride a.spss = sps_stride(r)):
-// [N1 (r4) | N2 (r4) | A[e1] (r4) | scalars (16)]
+// [N_{h,q} (r4 each, piece p = h NQ + q) | A[e1] (r4) | scalars (32)]
 enum {
     SPS_SZ = 0,      // sum_k P_k z_k (k_sp_enc)
-    SPS_LEFT,        // <V1, A[e1]>, <V2, A[e1]>      (k_sp_dec, side 0)
+    SPS_LEFT,        // <V1, A[e1]>, <V2, A[e1]>      (k_sp_dec piece 0)
     SPS_RIGHT,
     SPS_DU1,         // d cost / d u1, u2 (positive scores)
     SPS_DU2,
     SPS_LBASE,       // -softplus(-u1) - softplus(-u2) + 2 H
-    SPS_SDG1,        // side 0: sum of its coefficients, sum of its log sigmoids, <N1, V1>
-    SPS_SLS1,
-    SPS_NV1,
-    SPS_SDG2,        // side 1: the same for neg2 and V2
-    SPS_SLS2,
-    SPS_NV2
+    SPS_PIECE = 8    // + 3 p: piece p's sum of coefficients, of log sigmoids, <N_p, V_h>
 };
-__host__ __device__ inline int sps_stride(int r) { return 3 * align4(r) + 16; }
-// LDS of one k_sp_dec side: V1, V2, the 1 + s rows, dots / ids / Ab / coefficients, the row-sum
+__host__ __device__ inline int sps_stride(int r) { return (RAE_SPD_NP + 1) * align4(r) + 32; }
+__host__ __device__ inline int sps_oa(int r4) { return RAE_SPD_NP * r4; }          // A[e1]
+__host__ __device__ inline int sps_os(int r4) { return (RAE_SPD_NP + 1) * r4; }    // scalars
+__host__ __device__ inline int spd_neg_per_piece(int s) { return (s + RAE_SPD_NQ - 1) / RAE_SPD_NQ; }
+// LDS of one k_sp_dec piece: V1, V2, its 1 + ns rows, dots / ids / Ab / coefficients, the row-sum
 // partials (<= 8 groups) and the block-sum scratch
 __host__ __device__ inline int sp_dec_side_smem_floats(int r, int s) {
-    const int r4 = align4(r), s4 = align4(s + 2);
-    return 2 * r4 + (1 + s) * r4 + 4 * s4 + 8 * r4 + 64;
+    const int ns = spd_neg_per_piece(s), r4 = align4(r), s4 = align4(ns + 2);
+    return 2 * r4 + (1 + ns) * r4 + 4 * s4 + 8 * r4 + 64;
 }
 
 template <bool V4>
@@ -75,7 +80,7 @@ __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
         float x = 0.f;
         for (int k = threadIdx.x; k < m; k += RAE_WAVE) x += S.sP[k] * S.sZ[k];
         x = wave_sum(x);
-        if (threadIdx.x == 0) a.sps[(int64_t)bl * a.spss + 3 * align4(Dm.r) + SPS_SZ] = x;
+        if (threadIdx.x == 0) a.sps[(int64_t)bl * a.spss + sps_os(align4(Dm.r)) + SPS_SZ] = x;
     }
 }
 
@@ -112,9 +117,16 @@ __host__ __device__ inline int sp_cp_tasks(int l, int r) { return 2 * ((l + 15) 
 __host__ __device__ inline int sp_ctdw_tasks(int l, int m) { return ((l + 15) / 16) * ((m + 15) / 16); }
 
 // The two GEMMs: one 4-wave workgroup per 16 x 16 output tile; wave w takes the K chunks
-// c = w, w + 4, ... (16 deep each), four chunks' loads issued before their MFMAs, and the
+// c = w, w + 4, ... (16 deep each), RAE_SPG_U* chunks' loads issued before their MFMAs, and the
 // four waves' accumulators are combined in LDS in wave order (deterministic).
-#define RAE_SPG_U 4
+#ifndef RAE_SPG_UCP
+#define RAE_SPG_UCP 5   // k_sp_cp: 16-deep K chunks per wave per round (C4: m = 300, 19
+                        // chunks over 4 waves -- all in one round)
+#endif
+#ifndef RAE_SPG_UDW
+#define RAE_SPG_UDW 5   // k_sp_ctdw (C4: 2r = 600, 38 chunks, two rounds; measured forward
+                        // 28.0 us at 5, 28.7 at 10 (one round), 28.8 at 4)
+#endif
 __device__ __forceinline__ void sp_gemm_combine(rae_f32x4 acc, float* red, int lane, int w,
                                                 float out[4]) {
     float4* r4 = reinterpret_cast<float4*>(red);
@@ -147,16 +159,16 @@ __device__ void sp_split_cp(const StepArgs& a, int task, float* red) {
     const float* Cr = (which ? a.C2 : a.C1) + (int64_t)(iv ? i : 0) * m;
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int nch = (m + 15) / 16;
-    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
-        float4 x[RAE_SPG_U], y[RAE_SPG_U];
+    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_UCP) {
+        float4 x[RAE_SPG_UCP], y[RAE_SPG_UCP];
 #pragma unroll
-        for (int u = 0; u < RAE_SPG_U; ++u) {
+        for (int u = 0; u < RAE_SPG_UCP; ++u) {
             const int k = (c0 + u * RAE_NWAVE) * 16 + 4 * g;     // >= m past the last chunk
             x[u] = load4_guard<VEC>(Pr, k, m, bv);
             y[u] = load4_guard<VEC>(Cr, k, m, iv);
         }
 #pragma unroll
-        for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+        for (int u = 0; u < RAE_SPG_UCP; ++u) acc = mfma4_f32(x[u], y[u], acc);
     }
     float o[4];
     sp_gemm_combine(acc, red, lane, w, o);
@@ -251,12 +263,39 @@ __device__ void sp_vrec(const StepArgs& a, int task, int lane) {
     }
 }
 
+// the sums of an example's pieces (in piece order): side h's row sum N_h at column i, and the
+// scalars of side h (f = 0: coefficients, 1: log sigmoids, 2: <N, V_h>)
+__device__ __forceinline__ float sps_side(const float* scl, int h, int f) {
+    float v = scl[SPS_PIECE + 3 * (h * RAE_SPD_NQ) + f];
+#pragma unroll
+    for (int q = 1; q < RAE_SPD_NQ; ++q) v += scl[SPS_PIECE + 3 * (h * RAE_SPD_NQ + q) + f];
+    return v;
+}
+template <bool VEC>
+__device__ __forceinline__ float4 sps_rowsum4(const float* sp, int h, int i, int r, bool ok) {
+    const int r4 = align4(r);
+    float4 v = load4_guard<VEC>(sp + (h * RAE_SPD_NQ) * r4, i, r, ok);
+#pragma unroll
+    for (int q = 1; q < RAE_SPD_NQ; ++q) {
+        const float4 u = load4_guard<VEC>(sp + (h * RAE_SPD_NQ + q) * r4, i, r, ok);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    return v;
+}
+__device__ __forceinline__ float sps_rowsum(const float* sp, int h, int i, int r4) {
+    float v = sp[(h * RAE_SPD_NQ) * r4 + i];
+#pragma unroll
+    for (int q = 1; q < RAE_SPD_NQ; ++q) v += sp[(h * RAE_SPD_NQ + q) * r4 + i];
+    return v;
+}
+
 // k_sp_ctdw: tile (example, k) of dP.  A = dw (rows b, K = i: one float4 per lane per chunk,
-// assembled as it loads: dl A[e1] + N1 / dr A[e1] + N2), B = C (K = i rows, columns k: four
-// strided scalars per lane); K runs over C1's then C2's i.  Besides dS the tile stores, for its
-// 16 examples and the embedding columns i = 16 kt + (0..15) (+ 16 nkt q), dw1, dw2 (what the
-// update's dense tiles read) and G1 = dl V1 + dr V2 (or dl, dr for the wire record), and tile
-// kt = 0 the loss -- their loads issued before the GEMM, their stores after it.
+// assembled as it loads: dl A[e1] + N1 / dr A[e1] + N2, N_h the sum of the side's pieces), B = C
+// (K = i rows, columns k: four strided scalars per lane); K runs over C1's then C2's i.  Besides
+// dS the tile stores, for its 16 examples and the embedding columns i = 16 kt + (0..15)
+// (+ 16 nkt q), dw1, dw2 (what the update's dense tiles read) and G1 = dl V1 + dr V2 (or dl, dr
+// for the wire record), and tile kt = 0 the loss -- their loads issued before the GEMM, their
+// stores after it.
 template <bool VEC>
 __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int l = a.l, m = a.m, r = a.r, r4 = align4(r);
@@ -266,16 +305,18 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int li = lane & 15, g = lane >> 4;
     const int b = bt * 16 + li, k = kt * 16 + li;
     const bool bv = b < l, kv = k < m;
+    const int oS = sps_os(r4);
     float* sdl = red + RAE_BT * 4;                        // [16]: sd of the tile's examples
     // this lane's GEMM row (example b): dl, dr from both sides' sums
     const float* spb = a.sps + (int64_t)(bv ? b : 0) * a.spss;
-    const float* scb = spb + 3 * r4;
+    const float* scb = spb + oS;
     const float du1b = scb[SPS_DU1], du2b = scb[SPS_DU2];
-    const float dlb = du1b + du2b + scb[SPS_SDG2];      // as sp_coefficients: d cost / d left
-    const float drb = du1b + du2b + scb[SPS_SDG1];
+    const float dlb = du1b + du2b + sps_side(scb, 1, 0);  // as sp_coefficients: d cost / d left
+    const float drb = du1b + du2b + sps_side(scb, 0, 0);
     float lft = 0.f, rgt = 0.f, nv1 = 0.f, nv2 = 0.f;
     if (w == 0 && g == 0) {
-        lft = scb[SPS_LEFT]; rgt = scb[SPS_RIGHT]; nv1 = scb[SPS_NV1]; nv2 = scb[SPS_NV2];
+        lft = scb[SPS_LEFT]; rgt = scb[SPS_RIGHT];
+        nv1 = sps_side(scb, 0, 2); nv2 = sps_side(scb, 1, 2);
     }
     // the tile's stores of dw1, dw2, G1: pair (example eo, column ii) per thread
     const int pr = threadIdx.x, eo = pr >> 4, ii = pr & 15;
@@ -283,17 +324,19 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const bool sv = bo_s < l;
     const int bs = sv ? bo_s : 0;
     const float* sps_s = a.sps + (int64_t)bs * a.spss;
+    const float* scs = sps_s + oS;
     const int is0 = kt * 16 + ii;
     const bool iv0 = sv && is0 < r;
     const int ic0 = iv0 ? is0 : 0;
-    const float s_du1 = sps_s[3 * r4 + SPS_DU1], s_du2 = sps_s[3 * r4 + SPS_DU2];
-    const float s_sdg1 = sps_s[3 * r4 + SPS_SDG1], s_sdg2 = sps_s[3 * r4 + SPS_SDG2];
+    const float s_du1 = scs[SPS_DU1], s_du2 = scs[SPS_DU2];
+    const float s_sdg1 = sps_side(scs, 0, 0), s_sdg2 = sps_side(scs, 1, 0);
     const float* vrow = a.vb + (int64_t)(a.rank * l + bs) * a.vbs;
-    const float sa0 = sps_s[2 * r4 + ic0], sn10 = sps_s[ic0], sn20 = sps_s[r4 + ic0];
+    const float sa0 = sps_s[sps_oa(r4) + ic0];
+    const float sn10 = sps_rowsum(sps_s, 0, ic0, r4), sn20 = sps_rowsum(sps_s, 1, ic0, r4);
     const float sv10 = vrow[a.vV1 + ic0], sv20 = vrow[a.vV2 + ic0];
     const bool lossl = kt == 0 && ii == 0 && sv;
-    const float lbase = lossl ? sps_s[3 * r4 + SPS_LBASE] : 0.f;
-    const float sls = lossl ? sps_s[3 * r4 + SPS_SLS1] + sps_s[3 * r4 + SPS_SLS2] : 0.f;
+    const float lbase = lossl ? scs[SPS_LBASE] : 0.f;
+    const float sls = lossl ? sps_side(scs, 0, 1) + sps_side(scs, 1, 1) : 0.f;
     // the epilogue's operands (wave 0): P, z and sz of its four output rows
     const int kc = kv ? k : 0;
     float pk[4], zk[4], sz[4];
@@ -304,21 +347,21 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             const float* rec = a.ex + (int64_t)(a.rank * l + bo) * a.lay.rec;
             pk[reg] = rec[a.lay.oP + kc];
             zk[reg] = rec[a.lay.odS + kc];
-            sz[reg] = a.sps[(int64_t)bo * a.spss + 3 * r4 + SPS_SZ];
+            sz[reg] = a.sps[(int64_t)bo * a.spss + oS + SPS_SZ];
         }
     }
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int nci = (r + 15) / 16, nch = 2 * nci;
-    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_U) {
-        float4 x[RAE_SPG_U], y[RAE_SPG_U];
+    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_UDW) {
+        float4 x[RAE_SPG_UDW], y[RAE_SPG_UDW];
 #pragma unroll
-        for (int u = 0; u < RAE_SPG_U; ++u) {
+        for (int u = 0; u < RAE_SPG_UDW; ++u) {
             const int c = c0 + u * RAE_NWAVE;
             const bool cv = c < nch;
             const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
             const float* Cm = which ? a.C2 : a.C1;
-            const float4 nn = load4_guard<VEC>(spb + which * r4, i, r, bv && cv);
-            const float4 ae = load4_guard<VEC>(spb + 2 * r4, i, r, bv && cv);
+            const float4 nn = sps_rowsum4<VEC>(spb, which, i, r, bv && cv);
+            const float4 ae = load4_guard<VEC>(spb + sps_oa(r4), i, r, bv && cv);
             const float dd = which ? drb : dlb;
             x[u] = make_float4(fmaf(dd, ae.x, nn.x), fmaf(dd, ae.y, nn.y),
                                fmaf(dd, ae.z, nn.z), fmaf(dd, ae.w, nn.w));
@@ -333,7 +376,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             y[u].w = o3 ? c3 : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < RAE_SPG_U; ++u) acc = mfma4_f32(x[u], y[u], acc);
+        for (int u = 0; u < RAE_SPG_UDW; ++u) acc = mfma4_f32(x[u], y[u], acc);
     }
     // dw1, dw2 and G1 (the same fmaf forms as the GEMM operand and as k_vrec)
     {
@@ -346,9 +389,9 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
             if (!a.lay.wire) rec[a.lay.oG1 + is0] = fmaf(dl, sv10, dr * sv20);
         }
         for (int is = is0 + 16 * nkt; sv && is < r; is += 16 * nkt) {    // r > 16 nkt only
-            const float ae = sps_s[2 * r4 + is];
-            dwr[a.dw1o + is] = fmaf(dl, ae, sps_s[is]);
-            dwr[a.dw2o + is] = fmaf(dr, ae, sps_s[r4 + is]);
+            const float ae = sps_s[sps_oa(r4) + is];
+            dwr[a.dw1o + is] = fmaf(dl, ae, sps_rowsum(sps_s, 0, is, r4));
+            dwr[a.dw2o + is] = fmaf(dr, ae, sps_rowsum(sps_s, 1, is, r4));
             if (!a.lay.wire) rec[a.lay.oG1 + is] = fmaf(dl, vrow[a.vV1 + is], dr * vrow[a.vV2 + is]);
         }
         if (lossl) {
@@ -376,25 +419,28 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     }
 }
 
-// k_sp_dec, one side h of example bl: the A rows of e1 and of the side's s negatives by LDS-DMA
-// (half the example's gather), the dots <V1, A[e1]>, <V2, A[e1]> and <V_h, A[neg_h,t]>, the side's
-// coefficients (its record entries written here), its weighted row sum N_h and <N_h, V_h>; side
-// 0 also the positive scores' terms and a copy of A[e1].  The assembly dw = d A[e1] + N waits
-// for both sides: k_sp_ctdw.
+// k_sp_dec, piece q of side h of example bl: the A rows of e1 and of the piece's negatives of
+// that side by LDS-DMA, the dots <V1, A[e1]>, <V2, A[e1]> and <V_h, A[neg_h,t]>, the piece's
+// coefficients (its record entries written here), its weighted row sum N = sum_t dg_t A[neg_h,t]
+// and <N, V_h>; piece 0 of side 0 also the positive scores' terms and a copy of A[e1].  The
+// assembly dw = d A[e1] + N waits for every piece: k_sp_ctdw.
 template <bool V4>
-__device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* smem) {
+__device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char* smem) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
-    const int r = a.r, s = a.s, r4 = align4(r), rv = r / VW, r4v = r4 / VW, s4 = align4(s + 2);
-    const int NR = 1 + s;
+    const int r = a.r, s = a.s, r4 = align4(r), rv = r / VW, r4v = r4 / VW;
+    const int h = pc / RAE_SPD_NQ, q = pc - h * RAE_SPD_NQ;
+    const int nsp = spd_neg_per_piece(s), t0 = q * nsp;
+    const int nt = max(0, min(s - t0, nsp));                  // this piece's negatives
+    const int s4 = align4(nsp + 2), NR = 1 + nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float* p = reinterpret_cast<float*>(smem);
     float* sV1 = p; p += r4;
     float* sV2 = p; p += r4;
-    float* srows = p; p += NR * r4;
-    float* sdots = p; p += s4;            // [0] left, [1] right, [2 + t] negative t
-    float* sAb = p; p += s4;              // [0] e1, [1] e2, [2 + t] negative t
-    float* scf = p; p += s4;              // coefficient of negative t
+    float* srows = p; p += (1 + nsp) * r4;
+    float* sdots = p; p += s4;            // [0] left, [1] right, [2 + u] negative t0 + u
+    float* sAb = p; p += s4;              // [0] e1, [1] e2, [2 + u] negative t0 + u
+    float* scf = p; p += s4;              // coefficient of negative t0 + u
     int* sid = reinterpret_cast<int*>(p); p += s4;
     float* spart = p; p += 8 * r4;
     float* sred = p;
@@ -403,19 +449,20 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
     const int64_t col = a.neg_mode ? ex : (int64_t)bg;
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     float* sp = a.sps + (int64_t)bl * a.spss;
-    float* scl = sp + 3 * r4;
+    float* scl = sp + sps_os(r4);
+    const bool lead = pc == 0;                                // the positive terms, A[e1]
     RAE_STAMP(a, 0);
-    if (threadIdx.x < s + 2) {
+    if (threadIdx.x < nt + 2) {
         const int j = threadIdx.x;
         const int* src = j == 0 ? a.args1 + ex : j == 1 ? a.args2 + ex
-                       : (h ? a.neg2 : a.neg1) + (int64_t)(j - 2) * a.neg_stride + col;
+                       : (h ? a.neg2 : a.neg1) + (int64_t)(t0 + j - 2) * a.neg_stride + col;
         sid[j] = *src;
     }
-    const float H = (h == 0 && threadIdx.x == 0) ? rec[a.lay.oloss] : 0.f;
+    const float H = (lead && threadIdx.x == 0) ? rec[a.lay.oloss] : 0.f;
     __syncthreads();
     RAE_STAMP(a, 1);
-    if (threadIdx.x < s + 2) sAb[threadIdx.x] = a.Ab[sid[threadIdx.x]];
-    {   // rho 0: A[e1]; rho >= 1: negative rho - 1 (id slot rho + 1)
+    if (threadIdx.x < nt + 2) sAb[threadIdx.x] = a.Ab[sid[threadIdx.x]];
+    {   // rho 0: A[e1]; rho >= 1: negative t0 + rho - 1 (id slot rho + 1)
         const int nchunk = (rv + 63) / 64;
         for (int t = w; t < NR * nchunk; t += RAE_FNW) {
             const int rho = t / nchunk, ch = t - rho * nchunk;
@@ -437,36 +484,36 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
     }
     __syncthreads();                                          // the A-row DMA has landed
     RAE_STAMP(a, 2);
-    {   // dots, 16 lanes each (sp_dots' arithmetic): t = 0 left, 1 right, 2 + u negative u
+    {   // dots, 16 lanes each (sp_dots' arithmetic): t = 0 left, 1 right, 2 + u negative
         const VT* Rv = reinterpret_cast<const VT*>(srows);
         const VT* W1 = reinterpret_cast<const VT*>(sV1);
         const VT* W2 = reinterpret_cast<const VT*>(sV2);
         const VT* Wh = h ? W2 : W1;
-        const int ndot = s + 2;
+        const int ndot = nt + 2;
         for (int base = 0; base < ndot * 16; base += RAE_FBT) {
-            const int idx = base + threadIdx.x, t = idx >> 4, q = idx & 15;
+            const int idx = base + threadIdx.x, t = idx >> 4, qq = idx & 15;
             float d = 0.f;
             if (t < ndot) {
                 const VT* wv = t == 0 ? W1 : (t == 1 ? W2 : Wh);
                 const VT* x = Rv + (t < 2 ? 0 : t - 1) * r4v;
-                for (int c = q; c < rv; c += 16) d += vdot(x[c], wv[c]);
+                for (int c = qq; c < rv; c += 16) d += vdot(x[c], wv[c]);
             }
             d = group16_sum(d);
-            if (t < ndot && q == 0) sdots[t] = d;
+            if (t < ndot && qq == 0) sdots[t] = d;
         }
     }
     __syncthreads();
     RAE_STAMP(a, 3);
-    if (w == 0) {   // the side's coefficients (sp_coefficients' arithmetic), one wave
+    if (w == 0) {   // the piece's coefficients (sp_coefficients' arithmetic), one wave
         const float left = sdots[0], right = sdots[1], oth = h ? left : right;
         float sdg = 0.f, sls = 0.f;
-        for (int t = lane; t < s; t += RAE_WAVE) {
-            const float gg = sdots[2 + t] + oth + sAb[2 + t];
+        for (int u = lane; u < nt; u += RAE_WAVE) {
+            const float gg = sdots[2 + u] + oth + sAb[2 + u];
             float sg, spl;
             sigmoid_softplus(gg, sg, spl);
             const float dg = sg * a.invD;
-            scf[t] = dg;
-            const int j = 2 + h * s + t;
+            scf[u] = dg;
+            const int j = 2 + h * s + t0 + u;
             rec[a.lay.ocoef + 2 * j] = dg;
             rec[a.lay.ocoef + 2 * j + 1] = dg;
             sdg += dg;
@@ -475,9 +522,9 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
         sdg = wave_sum(sdg);
         sls = wave_sum(sls);
         if (lane == 0) {
-            scl[h ? SPS_SDG2 : SPS_SDG1] = sdg;
-            scl[h ? SPS_SLS2 : SPS_SLS1] = sls;
-            if (h == 0) {
+            scl[SPS_PIECE + 3 * pc + 0] = sdg;
+            scl[SPS_PIECE + 3 * pc + 1] = sls;
+            if (lead) {
                 const float one = left + right;
                 const float u1 = one + sAb[0], u2 = one + sAb[1];
                 float su1, pu1, su2, pu2;                     // sigmoid(-u), softplus(-u)
@@ -498,7 +545,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
     }
     __syncthreads();
     RAE_STAMP(a, 4);
-    // N_h = sum_t dg_t A[neg_h,t]: thread owns (vector column, row group), groups in fixed order
+    // N = sum_t dg_t A[neg_h,t]: thread owns (vector column, row group), groups in fixed order
     const int ngrp = RAE_FBT / rv > 8 ? 8 : (RAE_FBT / rv > 0 ? RAE_FBT / rv : 1);
     {
         const int grp = threadIdx.x / rv, c = threadIdx.x - grp * rv;
@@ -506,7 +553,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
             const VT* R = reinterpret_cast<const VT*>(srows);
             VT v;
             vzero(v);
-            for (int t = grp; t < s; t += ngrp) vfma(v, scf[t], R[(1 + t) * r4v + c]);
+            for (int u = grp; u < nt; u += ngrp) vfma(v, scf[u], R[(1 + u) * r4v + c]);
             reinterpret_cast<VT*>(spart)[grp * rv + c] = v;
         }
     }
@@ -517,12 +564,12 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int h, char* 
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
         float v = 0.f;
         for (int gg = 0; gg < ngrp; ++gg) v += spart[gg * r + i];
-        sp[h * r4 + i] = v;
+        sp[pc * r4 + i] = v;
         x1 += v * sVh[i];
-        if (h == 0) sp[2 * r4 + i] = srows[i];                // A[e1] for the assembly
+        if (lead) sp[sps_oa(r4) + i] = srows[i];              // A[e1] for the assembly
     }
     const float nv = block_sum<RAE_FBT>(x1, sred);
-    if (threadIdx.x == 0) scl[h ? SPS_NV2 : SPS_NV1] = nv;
+    if (threadIdx.x == 0) scl[SPS_PIECE + 3 * pc + 2] = nv;
     RAE_STAMP(a, 6);
     RAE_STAMP(a, 7);
 }
