@@ -424,6 +424,16 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
 // coefficients (its record entries written here), its weighted row sum N = sum_t dg_t A[neg_h,t]
 // and <N, V_h>; piece 0 of side 0 also the positive scores' terms and a copy of A[e1].  The
 // assembly dw = d A[e1] + N waits for every piece: k_sp_ctdw.
+// phase stamps (diagnostic builds): piece 0 of each example, at the example's slot
+#ifdef RAE_STAMPS
+#define SPD_STAMP(slot)                                                                     \
+    do {                                                                                    \
+        if (a.stamps && threadIdx.x == 0 && pc == 0)                                        \
+            a.stamps[(size_t)bl * 16 + (slot)] = __builtin_amdgcn_s_memrealtime();          \
+    } while (0)
+#else
+#define SPD_STAMP(slot) do { } while (0)
+#endif
 template <bool V4>
 __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char* smem) {
     typedef typename VecT<V4>::T VT;
@@ -451,7 +461,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
     float* sp = a.sps + (int64_t)bl * a.spss;
     float* scl = sp + sps_os(r4);
     const bool lead = pc == 0;                                // the positive terms, A[e1]
-    RAE_STAMP(a, 0);
+    SPD_STAMP(0);
     if (threadIdx.x < nt + 2) {
         const int j = threadIdx.x;
         const int* src = j == 0 ? a.args1 + ex : j == 1 ? a.args2 + ex
@@ -460,7 +470,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
     }
     const float H = (lead && threadIdx.x == 0) ? rec[a.lay.oloss] : 0.f;
     __syncthreads();
-    RAE_STAMP(a, 1);
+    SPD_STAMP(1);
     if (threadIdx.x < nt + 2) sAb[threadIdx.x] = a.Ab[sid[threadIdx.x]];
     {   // rho 0: A[e1]; rho >= 1: negative t0 + rho - 1 (id slot rho + 1)
         const int nchunk = (rv + 63) / 64;
@@ -483,7 +493,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
         sV2[i] = vrow[a.vV2 + i];
     }
     __syncthreads();                                          // the A-row DMA has landed
-    RAE_STAMP(a, 2);
+    SPD_STAMP(2);
     {   // dots, 16 lanes each (sp_dots' arithmetic): t = 0 left, 1 right, 2 + u negative
         const VT* Rv = reinterpret_cast<const VT*>(srows);
         const VT* W1 = reinterpret_cast<const VT*>(sV1);
@@ -503,7 +513,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
         }
     }
     __syncthreads();
-    RAE_STAMP(a, 3);
+    SPD_STAMP(3);
     if (w == 0) {   // the piece's coefficients (sp_coefficients' arithmetic), one wave
         const float left = sdots[0], right = sdots[1], oth = h ? left : right;
         float sdg = 0.f, sls = 0.f;
@@ -544,7 +554,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
         }
     }
     __syncthreads();
-    RAE_STAMP(a, 4);
+    SPD_STAMP(4);
     // N = sum_t dg_t A[neg_h,t]: thread owns (vector column, row group), groups in fixed order
     const int ngrp = RAE_FBT / rv > 8 ? 8 : (RAE_FBT / rv > 0 ? RAE_FBT / rv : 1);
     {
@@ -558,7 +568,7 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
         }
     }
     __syncthreads();
-    RAE_STAMP(a, 5);
+    SPD_STAMP(5);
     const float* sVh = h ? sV2 : sV1;
     float x1 = 0.f;
     for (int i = threadIdx.x; i < r; i += RAE_FBT) {
@@ -570,8 +580,8 @@ __device__ void sp_split_dec(const StepArgs& a, int64_t g, int bl, int pc, char*
     }
     const float nv = block_sum<RAE_FBT>(x1, sred);
     if (threadIdx.x == 0) scl[SPS_PIECE + 3 * pc + 2] = nv;
-    RAE_STAMP(a, 6);
-    RAE_STAMP(a, 7);
+    SPD_STAMP(6);
+    SPD_STAMP(7);
 }
 
 }  // namespace rae

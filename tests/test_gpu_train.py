@@ -139,11 +139,14 @@ def test_synthetic_vs_oracle(built_lib, cuda_dev, shape):
     dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5, force=True),      # scalar path
     dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10, force=True),
     dict(N=200, d=3000, m=300, r=300, s=50, l=100, ntrue=10, epochs=1),  # C4 K/r/s: split by default
-], ids=["small", "odd", "c3shape", "c4shape"])
+    # r > 16 ceil(m / 16): k_sp_ctdw's tiles store dw / G1 over several column strides; l not a
+    # multiple of 16, odd s
+    dict(N=300, d=500, m=8, r=44, s=5, l=37, ntrue=4, force=True),
+], ids=["small", "odd", "c3shape", "c4shape", "wide"])
 def test_split_sp_forward_vs_oracle(built_lib, cuda_dev, shape):
-    """The split SP forward (rae_sp_split.hpp: encoder, P.C^T GEMM, decoder, dw.C GEMM,
-    softmax backward as five kernels) against the float64 oracle, with the same tolerances as
-    the fused example kernel."""
+    """The split SP forward (rae_sp_split.hpp: encoder, P.C^T GEMM, decoder per negative side,
+    dw.C GEMM with the softmax backward in its epilogue) against the float64 oracle, with the
+    same tolerances as the fused example kernel."""
     from rae.data import synthetic_dataset
     from rae.inducer import ReconstructInducer
     forms = {"sp_forward": "split"} if shape.get("force") else {}
