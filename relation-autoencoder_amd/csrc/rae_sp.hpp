@@ -341,6 +341,9 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     const VT* Wv = reinterpret_cast<const VT*>(a.W);
     VT acc;
     vzero(acc);
+    // the bias entry this thread adds below (mp <= RAE_FBT: one per thread), loaded now so it is
+    // not a dependent round trip behind the W rows' barrier
+    const float wb0 = (threadIdx.x < m) ? a.Wb[threadIdx.x] : 0.f;
     bool issued = false;
     for (int pc = p0; pc < p1; pc += RAE_FBT) {
         const int nf = min(RAE_FBT, p1 - pc);
@@ -386,7 +389,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         float v = 0.f;
         if (k < m) {
             for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
-            v += a.Wb[k];
+            v += k == (int)threadIdx.x ? wb0 : a.Wb[k];
         }
         sS[k] = v;
     }
@@ -648,6 +651,9 @@ template <bool V4, class D>
 __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     const D Dm(a);
     const int m = Dm.m, r = Dm.r, s = Dm.s, NR = 1 + 2 * s;
+    // the r-vectors (A rows, V, dw) go four wide whenever r allows, independent of m (C2:
+    // m = 30, r = 100)
+    constexpr bool VR = V4 || (D::fixed && DimT<D>::r % 4 == 0);
     const int r4 = align4(r), mp = pad_m(m);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     ExampleSmem S = carve_example_smem(smem, 0, m, r, s);
@@ -673,14 +679,14 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 1);
     const int NJ = 2 + 2 * s;
     if (threadIdx.x < NJ) S.sAbv[threadIdx.x] = a.Ab[S.sids[threadIdx.x]];
-    encoder_forward<V4, V4, kLoadC>(a, Dm, S, NR, 1, cc_, true);
+    encoder_forward<V4, VR, kLoadC>(a, Dm, S, NR, 1, cc_, true);
     const float H = S.sred[40];
     RAE_STAMP(a, 2);
     sp_project<V4>(a, Dm, S, cc_);
     __syncthreads();
     RAE_STAMP(a, 3);
 
-    sp_dots<V4>(Dm, S);
+    sp_dots<VR>(Dm, S);
     __syncthreads();
     RAE_STAMP(a, 4);
 
@@ -690,7 +696,7 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 8);
 
     // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
-    sp_weighted_rows<V4>(Dm, S);
+    sp_weighted_rows<VR>(Dm, S);
     for (int k = threadIdx.x; k < mp; k += RAE_FBT) S.sdP[k] = 0.f;
     __syncthreads();
     RAE_STAMP(a, 5);
