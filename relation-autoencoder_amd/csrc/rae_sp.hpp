@@ -326,7 +326,14 @@ __device__ __forceinline__ void sp_project_back(const StepArgs& a, const D& Dm, 
 #ifndef RAE_ENC_KF
 #define RAE_ENC_KF 4
 #endif
-template <bool V4, bool V4R, bool LOADC, class D, class Cache>
+// encoder phase stamps (diagnostic builds, slots 10-13): only the split forward's k_sp_enc
+// records them (RAE_ENC_STAMPS there), the fused paths keep those slots for their own
+#if defined(RAE_STAMPS)
+#define RAE_ESTAMP(a, slot) do { if (ESTAMP) RAE_STAMP(a, slot); } while (0)
+#else
+#define RAE_ESTAMP(a, slot) do { } while (0)
+#endif
+template <bool V4, bool V4R, bool LOADC, class D, class Cache, bool ESTAMP = false>
 __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, ExampleSmem& S,
                                                 int NR, int skip_e2, Cache& cc_,
                                                 bool desc = false) {
@@ -352,6 +359,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
             S.sfval[threadIdx.x] = a.values ? a.values[pc + threadIdx.x] : 1.f;
         }
         __syncthreads();
+        RAE_ESTAMP(a, 10);
         if (!issued) gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
         if (slot < nslot) {
             // RAE_ENC_KF rows' loads in flight per round (the feature order of the sum is kept):
@@ -384,6 +392,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     VT* part = reinterpret_cast<VT*>(S.spart);
     if (slot < nslot && mv <= RAE_FBT) part[slot * mv + c] = acc;
     __syncthreads();
+    RAE_ESTAMP(a, 11);
     float* sS = S.sdP;
     for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
         float v = 0.f;
@@ -394,29 +403,49 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         sS[k] = v;
     }
     __syncthreads();
+    RAE_ESTAMP(a, 12);
     const int lane = threadIdx.x & 63;
     if (m <= 8 * RAE_WAVE) {
         if (threadIdx.x < RAE_WAVE) {                      // wave 0: no block barriers
+            // the lane's scores in registers, one exp each (fast_softmax's form: P = e / sum e
+            // as e * (1 / sum e)); also sum_k P_k z_k (S.sred[41], the split forward's sz)
+            float sv[8], ev[8];
             float mx = -INFINITY;
-            for (int k = lane; k < m; k += RAE_WAVE) mx = fmaxf(mx, sS[k]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + RAE_WAVE * i;
+                sv[i] = k < m ? sS[k] : 0.f;
+                if (k < m) mx = fmaxf(mx, sv[i]);
+            }
             mx = wave_max(mx);
             float se = 0.f;
-            for (int k = lane; k < m; k += RAE_WAVE) se += __expf(sS[k] - mx);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + RAE_WAVE * i;
+                ev[i] = k < m ? __expf(sv[i] - mx) : 0.f;
+                se += ev[i];
+            }
             se = wave_sum(se);
-            const float lse = __logf(se);
-            float hp = 0.f;
-            for (int k = lane; k < mp; k += RAE_WAVE) {
-                float z = 0.f, p = 0.f;
-                if (k < m) {
-                    z = sS[k] - mx;
-                    p = __expf(z) / se;
+            const float inv = 1.f / se, lse = __logf(se);
+            float hp = 0.f, zp = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + RAE_WAVE * i;
+                const float z = k < m ? sv[i] - mx : 0.f;
+                const float p = ev[i] * inv;
+                if (k < mp) {
+                    S.sZ[k] = z;
+                    S.sP[k] = p;
                 }
-                S.sZ[k] = z;
-                S.sP[k] = p;
                 hp += p * (z - lse);
+                zp += p * z;
             }
             hp = wave_sum(hp);
-            if (lane == 0) S.sred[40] = -a.alpha * hp;
+            zp = wave_sum(zp);
+            if (lane == 0) {
+                S.sred[40] = -a.alpha * hp;
+                S.sred[41] = zp;
+            }
         }
     } else {
         float mx = -INFINITY;
@@ -441,6 +470,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         if (threadIdx.x == 0) S.sred[40] = -a.alpha * hp;
     }
     __syncthreads();
+    RAE_ESTAMP(a, 13);
 }
 
 // entropy term + softmax backward.  With d = the decoder's dCost/dP and the entropy's

@@ -66,22 +66,28 @@ __device__ void sp_split_enc(const StepArgs& a, int64_t g, int bl, char* smem) {
     ExampleSmem S = carve_example_smem(smem, 0, m, Dm.r, 0);      // no A rows here
     const int bg = a.rank * a.l + bl;
     const int64_t ex = g * (int64_t)a.L + bg;
+    RAE_STAMP(a, 8);
     load_desc(a, Dm, g, bl, S, false);
     __syncthreads();
+    RAE_STAMP(a, 9);
     CCache<V4, DynDims> cc_;                                       // unused: no C here
-    encoder_forward<V4, V4, false>(a, Dm, S, 0, 1, cc_, true);
+    encoder_forward<V4, V4, false, DynDims, CCache<V4, DynDims>, true>(a, Dm, S, 0, 1, cc_, true);
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     for (int k = threadIdx.x; k < m; k += RAE_FBT) {
         rec[a.lay.oP + k] = S.sP[k];
         rec[a.lay.odS + k] = S.sZ[k];
     }
-    if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[40];
-    if (threadIdx.x < RAE_WAVE) {                // sz = sum_k P_k z_k for k_sp_ctdw's epilogue
-        float x = 0.f;
-        for (int k = threadIdx.x; k < m; k += RAE_WAVE) x += S.sP[k] * S.sZ[k];
-        x = wave_sum(x);
-        if (threadIdx.x == 0) a.sps[(int64_t)bl * a.spss + sps_os(align4(Dm.r)) + SPS_SZ] = x;
+    if (threadIdx.x == 0) {
+        rec[a.lay.oloss] = S.sred[40];
+        // sz = sum_k P_k z_k for k_sp_ctdw's epilogue (the encoder's wave 0 for m <= 512)
+        float x = S.sred[41];
+        if (m > 8 * RAE_WAVE) {
+            x = 0.f;
+            for (int k = 0; k < m; ++k) x += S.sP[k] * S.sZ[k];
+        }
+        a.sps[(int64_t)bl * a.spss + sps_os(align4(Dm.r)) + SPS_SZ] = x;
     }
+    RAE_STAMP(a, 14);
 }
 
 // four fp32 MFMAs over a 16-deep K chunk: lane (li, g) supplies K = k0 + 4g + j for MFMA j

@@ -111,7 +111,8 @@ def main():
     names = {"A-index": ["enumerate", "sort", "segment"], "W-index": ["enumerate", "sort", "segment"],
              "example": ["ids+C-cache", "encoder+gather", "C.P", "dots", "coef+dwC", "back+softmax",
                          "record"]}
-    if cfg["dec"] == "sp" and cfg["r"] * cfg["m"] > 32768:      # split forward: k_sp_dec's stamps
+    split = cfg["dec"] == "sp" and cfg["r"] * cfg["m"] > 32768
+    if split:                                                    # split forward: k_sp_dec's stamps
         names["example"] = ["ids", "A-DMA+V", "dots", "coef", "weighted-rows", "record", "-"]
     spans = []
     for kind, sl in kinds.items():
@@ -134,7 +135,15 @@ def main():
         print(f"  sub-phases: coef {np.median(sub[:, 8] - sub[:, 4]):.2f}  weighted-rows "
               f"{np.median(sub[:, 5] - sub[:, 8]):.2f}  C^T.dw {np.median(sub[:, 9] - sub[:, 5]):.2f}"
               f"  softmax-bwd {np.median(sub[:, 6] - sub[:, 9]):.2f}")
-    if np.all(sub[:, 13] > 0) and np.all(sub[:, 12] > 0):
+    if split and np.all(sub[:, 14] > 0):
+        # k_sp_enc (slots 8-14): descriptor, feature ids, W rows + partial sums, S, softmax, record
+        e = sub[:, 8:15]
+        t0 = e[:, 0].min()
+        print("  k_sp_enc: start {:.2f}/{:.2f}  desc {:.2f}  features {:.2f}  W-rows {:.2f}  S {:.2f}  "
+              "softmax {:.2f}  record {:.2f}  end {:.2f}".format(
+                  np.median(e[:, 0] - t0), np.max(e[:, 0] - t0),
+                  *[np.median(e[:, q + 1] - e[:, q]) for q in range(6)], np.median(e[:, 6] - t0)))
+    elif np.all(sub[:, 13] > 0) and np.all(sub[:, 12] > 0):
         print(f"  fast-path encoder: indices {np.median(sub[:, 10] - sub[:, 1]):.2f}  W-issue "
               f"{np.median(sub[:, 11] - sub[:, 10]):.2f}  W-wait+FMA(wave0) {np.median(sub[:, 12] - sub[:, 11]):.2f}"
               f"  barrier {np.median(sub[:, 13] - sub[:, 12]):.2f}  S+softmax {np.median(sub[:, 2] - sub[:, 13]):.2f}")
@@ -142,10 +151,11 @@ def main():
         print(f"  icache test: coef rep0 {np.median(sub[:, 10] - sub[:, 4]):.2f}  rep1 "
               f"{np.median(sub[:, 11] - sub[:, 10]):.2f}")
     clk = []
-    for f in fw:
+    for f in ([] if split else fw):
         ex = f[HA + HW:gf]
         clk += list((ex[:, 15] - ex[:, 14]) * 100.0 / ((ex[:, 7] - ex[:, 0]) * 100.0) * 100.0 / 100.0)
-    print(f"  example-WG shader clock (s_memtime ticks / s_memrealtime): median {np.median(clk) * 100:.0f} MHz")
+    if clk:
+        print(f"  example-WG shader clock (s_memtime ticks / s_memrealtime): median {np.median(clk) * 100:.0f} MHz")
     tnames = ["C-tile", "R-tile", "Wb-tile", "cost", "A-row", "W-row", "A-heavy", "W-heavy",
               "A-vheavy", "W-vheavy"]
     allw = np.concatenate(up)
