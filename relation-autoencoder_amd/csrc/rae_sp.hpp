@@ -486,16 +486,26 @@ __device__ __forceinline__ void softmax_backward(const StepArgs& a, const D& Dm,
     const float ce = 2.f * a.alpha * a.invD;
     const int lane = threadIdx.x & 63;
     if (m <= 8 * RAE_WAVE) {
-        if (threadIdx.x < RAE_WAVE) {
+        if (threadIdx.x < RAE_WAVE) {                  // the lane's entries in registers
+            float pk[8], dk[8], zk[8];
             float sd = 0.f, sz = 0.f;
-            for (int k = lane; k < m; k += RAE_WAVE) {
-                sd += S.sP[k] * S.sdP[k];
-                sz += S.sP[k] * S.sZ[k];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + RAE_WAVE * i;
+                const bool in = k < m;
+                pk[i] = in ? S.sP[k] : 0.f;
+                dk[i] = in ? S.sdP[k] : 0.f;
+                zk[i] = in ? S.sZ[k] : 0.f;
+                sd += pk[i] * dk[i];
+                sz += pk[i] * zk[i];
             }
             sd = wave_sum(sd);
             sz = wave_sum(sz);
-            for (int k = lane; k < m; k += RAE_WAVE)
-                S.sdP[k] = S.sP[k] * ((S.sdP[k] - sd) + ce * (S.sZ[k] - sz));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + RAE_WAVE * i;
+                if (k < m) S.sdP[k] = pk[i] * ((dk[i] - sd) + ce * (zk[i] - sz));
+            }
         }
     } else {
         float sd = 0.f, sz = 0.f;
@@ -512,18 +522,22 @@ __device__ __forceinline__ void softmax_backward(const StepArgs& a, const D& Dm,
 }
 
 // write the common part of the exchange record
+// t0 / nt: the threads that write (thread t0 + u strides by nt); with_p: also P and dS
 template <class D>
 __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, ExampleSmem& S,
-                                             int bg) {
+                                             int bg, int t0 = 0, int nt = RAE_FBT,
+                                             bool with_p = true) {
     float* rec = a.ex + (int64_t)bg * a.lay.rec;
     float* dwr = a.dwb + (int64_t)bg * a.dws;
     const int m = Dm.m, r = Dm.r, NJ = 2 + 2 * Dm.s;
-    for (int k = threadIdx.x; k < m; k += RAE_FBT) {
-        rec[a.lay.oP + k] = S.sP[k];
-        rec[a.lay.odS + k] = S.sdP[k];
-    }
+    const int tid = (int)threadIdx.x - t0;
+    if (with_p)
+        for (int k = tid; k < m; k += nt) {
+            rec[a.lay.oP + k] = S.sP[k];
+            rec[a.lay.odS + k] = S.sdP[k];
+        }
     const float dl = S.scoef[0], dr = S.scoef[1];
-    for (int i = threadIdx.x; i < r; i += RAE_FBT) {
+    for (int i = tid; i < r; i += nt) {
         const float w1 = S.swC1[i], w2 = S.swC2[i];
         dwr[a.dw1o + i] = S.sdw1[i];
         dwr[a.dw2o + i] = S.sdw2[i];
@@ -537,13 +551,55 @@ __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, Exa
         rec[a.lay.oAux + 0] = dl;
         rec[a.lay.oAux + 1] = dr;
     }
-    for (int j = threadIdx.x; j < NJ; j += RAE_FBT) {
+    for (int j = tid; j < NJ; j += nt) {
         const float* c = S.scoef + 3 * j;
         const float cj = j == 0 ? 1.f : (j == 1 ? 0.f : (j < 2 + Dm.s ? c[0] : c[1]));
         rec[a.lay.ocoef + 2 * j] = cj;
         rec[a.lay.ocoef + 2 * j + 1] = c[2];
     }
-    if (threadIdx.x == 0) rec[a.lay.oloss] = S.sred[32];
+    if (tid == 0) rec[a.lay.oloss] = S.sred[32];
+}
+
+// softmax backward and the record, overlapped (m <= 512): wave 0 computes dS from registers and
+// stores P and dS straight into the record while waves 1.. write the rest of it
+template <class D>
+__device__ __forceinline__ void softmax_backward_record(const StepArgs& a, const D& Dm,
+                                                        ExampleSmem& S, int bg) {
+    const int m = Dm.m;
+    if (m > 8 * RAE_WAVE) {
+        softmax_backward(a, Dm, S);
+        write_record(a, Dm, S, bg);
+        return;
+    }
+    if (threadIdx.x >= RAE_WAVE) {
+        write_record(a, Dm, S, bg, RAE_WAVE, RAE_FBT - RAE_WAVE, false);
+        return;
+    }
+    const int lane = threadIdx.x;
+    const float ce = 2.f * a.alpha * a.invD;
+    float* rec = a.ex + (int64_t)bg * a.lay.rec;
+    float pk[8], dk[8], zk[8];
+    float sd = 0.f, sz = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                      // softmax_backward's arithmetic
+        const int k = lane + RAE_WAVE * i;
+        const bool in = k < m;
+        pk[i] = in ? S.sP[k] : 0.f;
+        dk[i] = in ? S.sdP[k] : 0.f;
+        zk[i] = in ? S.sZ[k] : 0.f;
+        sd += pk[i] * dk[i];
+        sz += pk[i] * zk[i];
+    }
+    sd = wave_sum(sd);
+    sz = wave_sum(sz);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        if (k < m) {
+            rec[a.lay.oP + k] = pk[i];
+            rec[a.lay.odS + k] = pk[i] * ((dk[i] - sd) + ce * (zk[i] - sz));
+        }
+    }
 }
 
 // v1[i] = c_a * row0[i] + sum_t coef1_t * rowsA_t[i],  v2 likewise (sums in t order):
@@ -732,9 +788,8 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 5);
     sp_project_back<V4>(a, Dm, S, cc_);
     RAE_STAMP(a, 9);
-    softmax_backward(a, Dm, S);
+    softmax_backward_record(a, Dm, S, bg);
     RAE_STAMP(a, 6);
-    write_record(a, Dm, S, bg);
     RAE_STAMP(a, 7);
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
