@@ -547,7 +547,7 @@ __device__ __forceinline__ void write_record(const StepArgs& a, const D& Dm, Exa
             rec[a.lay.oG1 + i] = dl * w1 + dr * w2;    // A[e1]: left and right both read it
         }
     }
-    if (a.lay.wire && threadIdx.x == 0) {
+    if (a.lay.wire && tid == 0) {
         rec[a.lay.oAux + 0] = dl;
         rec[a.lay.oAux + 1] = dr;
     }
@@ -723,6 +723,80 @@ __device__ __forceinline__ void sp_coefficients(const StepArgs& a, const D& Dm, 
     }
 }
 
+// sp_coefficients + sp_weighted_rows for s <= 32 and r-vectors of <= 64 columns, without their
+// two barriers and LDS hand-offs (the fast path's form): every wave computes the scores'
+// coefficients in registers (lanes t: neg1[t], lanes 32 + t: neg2[t]); wave 0 also leaves them
+// in S.scoef / S.sred[32] for the record; waves 0 / 1 sum dw1 / dw2 one vector column per lane,
+// the coefficients broadcast by readlane, in record order; the other waves clear S.sdP.  Ends
+// with the block barrier.
+template <bool VR, class D>
+__device__ __forceinline__ void sp_coef_rows_regs(const StepArgs& a, const D& Dm, ExampleSmem& S,
+                                                  float H) {
+    typedef typename VecT<VR>::T VT;
+    constexpr int VW = VR ? 4 : 1;
+    const int s = Dm.s, r4v = align4(Dm.r) / VW, rv = Dm.r / VW, mp = pad_m(Dm.m);
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float left = S.sdots[0], right = S.sdots[1];
+    const int tq = lane & 31;
+    const bool hi = lane >= 32;
+    float dg = 0.f, ls = 0.f;
+    if (tq < s) {
+        const int j = 2 + (hi ? s : 0) + tq;
+        const float gg = S.sdots[j] + (hi ? left : right) + S.sAbv[j];
+        float sg, spl;
+        sigmoid_softplus(gg, sg, spl);
+        dg = sg * a.invD;
+        ls = -spl;                                     // log sigmoid(-g) = -softplus(g)
+    }
+    float hs = group16_sum(dg);
+    hs += __uint_as_float(xor16_u32(__float_as_uint(hs)));
+    const float other = __uint_as_float(xor32_u32(__float_as_uint(hs)));
+    const float sdg1 = hi ? other : hs, sdg2 = hi ? hs : other;
+    const float one = left + right;
+    const float u1 = one + S.sAbv[0], u2 = one + S.sAbv[1];
+    float su1, spu1, su2, spu2;                        // sigmoid(-u), softplus(-u)
+    sigmoid_softplus(-u1, su1, spu1);
+    sigmoid_softplus(-u2, su2, spu2);
+    const float du1 = -su1 * a.invD, du2 = -su2 * a.invD;
+    const float dl = du1 + du2 + sdg2;                 // d cost / d left
+    const float dr = du1 + du2 + sdg1;                 // d cost / d right
+    if (w < 2) {
+        const VT* R = reinterpret_cast<const VT*>(S.srows);
+        const float c0 = w == 0 ? dl : dr;
+        const int off = w == 0 ? 0 : s;
+        if (w == 0) {                                  // the record's coefficients and loss
+            if (tq < s) {
+                float* c = S.scoef + 3 * (2 + (hi ? s : 0) + tq);
+                c[0] = hi ? 0.f : dg;
+                c[1] = hi ? dg : 0.f;
+                c[2] = dg;
+            }
+            const float sls = wave_sum(ls);
+            if (lane == 0) {
+                S.scoef[0] = dl; S.scoef[1] = dr; S.scoef[2] = du1;
+                S.scoef[3] = 0.f; S.scoef[4] = 0.f; S.scoef[5] = du2;
+                S.sred[32] = -spu1 - spu2 + 2.f * H + sls;
+            }
+        }
+        // branch-free (lanes past the row work on column 0, not stored): every readlane runs
+        // with the whole wave active -- a source lane outside EXEC has no defined value
+        const int lc = lane < rv ? lane : 0;
+        VT v;
+        vzero(v);
+        vfma(v, c0, R[lc]);
+        for (int t = 0; t < s; ++t) {
+            const float ct = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg),
+                                                                       (w == 0 ? 0 : 32) + t));
+            vfma(v, ct, R[(1 + off + t) * r4v + lc]);
+        }
+        if (lane < rv) reinterpret_cast<VT*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
+    } else {
+        for (int k = threadIdx.x - 2 * RAE_WAVE; k < mp; k += RAE_FBT - 2 * RAE_WAVE) S.sdP[k] = 0.f;
+    }
+    __syncthreads();
+}
+
 // ---- the SP example path ---------------------------------------------------------------
 #ifndef RAE_FWD_PFLAG
 #define RAE_FWD_PFLAG 1      // fast path: P published by an LDS flag, not a block barrier
@@ -777,14 +851,19 @@ __device__ void sp_example(const StepArgs& a, int64_t g, int bl, char* smem) {
     RAE_STAMP(a, 4);
 
     // scores, loss, coefficients (wave 0)
-    sp_coefficients(a, Dm, S, H);
-    __syncthreads();
-    RAE_STAMP(a, 8);
-
-    // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
-    sp_weighted_rows<VR>(Dm, S);
-    for (int k = threadIdx.x; k < mp; k += RAE_FBT) S.sdP[k] = 0.f;
-    __syncthreads();
+    if (s <= 32 && r / (VR ? 4 : 1) <= RAE_WAVE) {
+        // coefficients in every wave's registers and dw1 / dw2 by waves 0 / 1 (one barrier)
+        sp_coef_rows_regs<VR>(a, Dm, S, H);
+        RAE_STAMP(a, 8);
+    } else {
+        sp_coefficients(a, Dm, S, H);
+        __syncthreads();
+        RAE_STAMP(a, 8);
+        // dwC1 = dl*a1 + sum_t dg1_t n1_t ; dwC2 = dr*a1 + sum_t dg2_t n2_t
+        sp_weighted_rows<VR>(Dm, S);
+        for (int k = threadIdx.x; k < mp; k += RAE_FBT) S.sdP[k] = 0.f;
+        __syncthreads();
+    }
     RAE_STAMP(a, 5);
     sp_project_back<V4>(a, Dm, S, cc_);
     RAE_STAMP(a, 9);
@@ -1181,14 +1260,17 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     if (w < 2) {
         const float c0 = w == 0 ? dl : dr;
         float4 v = z4;
-        if (lv) {
-            vfma(v, c0, Rv[lane]);
+        // branch-free over the lanes (lc: lanes past the row re-read column 0, not stored), so
+        // every readlane runs with the whole wave active -- a source lane outside EXEC has no
+        // defined value
+        vfma(v, c0, Rv[lc]);
 #pragma unroll
-            for (int t = 0; t < s; ++t) {
-                const float ct = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg),
-                                                                           (w == 0 ? 0 : 32) + t));
-                vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lane]);
-            }
+        for (int t = 0; t < s; ++t) {
+            const float ct = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg),
+                                                                       (w == 0 ? 0 : 32) + t));
+            vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lc]);
+        }
+        if (lv) {
             reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
             rec_st(reinterpret_cast<float4*>(a.dwb + (int64_t)bg * a.dws + (w == 0 ? a.dw1o : a.dw2o)) + lane, v);
         }
