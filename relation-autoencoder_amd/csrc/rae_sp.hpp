@@ -348,17 +348,29 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     const VT* Wv = reinterpret_cast<const VT*>(a.W);
     VT acc;
     vzero(acc);
-    // the bias entry this thread adds below (mp <= RAE_FBT: one per thread), loaded now so it is
-    // not a dependent round trip behind the W rows' barrier
-    const float wb0 = (threadIdx.x < m) ? a.Wb[threadIdx.x] : 0.f;
+    const int lane = threadIdx.x & 63;
+    const bool w0 = threadIdx.x < RAE_WAVE;
+    // the bias entries S adds (wave 0's for m <= 512, one per thread otherwise), loaded now so
+    // they are not a dependent round trip behind the W rows' barrier
+    float wbk[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = lane + RAE_WAVE * i;
+        wbk[i] = (w0 && k < m && m <= 8 * RAE_WAVE) ? a.Wb[k] : 0.f;
+    }
+    const float wb0 = (m > 8 * RAE_WAVE && threadIdx.x < m) ? a.Wb[threadIdx.x] : 0.f;
+    const bool vals = a.values != nullptr;
     bool issued = false;
     for (int pc = p0; pc < p1; pc += RAE_FBT) {
         const int nf = min(RAE_FBT, p1 - pc);
-        if (threadIdx.x < nf) {
-            if (!have) S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
-            S.sfval[threadIdx.x] = a.values ? a.values[pc + threadIdx.x] : 1.f;
+        // binary features whose ids came with the descriptor: nothing to stage, no barrier
+        if (!have || vals) {
+            if (threadIdx.x < nf) {
+                if (!have) S.sfidx[threadIdx.x] = a.indices[pc + threadIdx.x];
+                S.sfval[threadIdx.x] = vals ? a.values[pc + threadIdx.x] : 1.f;
+            }
+            __syncthreads();
         }
-        __syncthreads();
         RAE_ESTAMP(a, 10);
         if (!issued) gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
         if (slot < nslot) {
@@ -374,7 +386,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
                         const int f = f0 + u * nslot;
                         const bool ok = f < nf;
                         wv[u] = Wv[(int64_t)S.sfidx[ok ? f : f0] * mv + cc];
-                        fv[u] = ok ? S.sfval[f] : 0.f;
+                        fv[u] = ok ? (vals ? S.sfval[f] : 1.f) : 0.f;
                     }
 #pragma unroll
                     for (int u = 0; u < RAE_ENC_KF; ++u)
@@ -383,7 +395,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
         }
         if (LOADC && !issued) cc_.load(a, Dm, 0, 0);         // behind the W-row loads
         issued = true;
-        __syncthreads();
+        if (pc + RAE_FBT < p1) __syncthreads();             // the next chunk restages
     }
     if (!issued) {
         gather_rows_dma<V4R>(a, Dm, S, NR, skip_e2);
@@ -394,28 +406,35 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     __syncthreads();
     RAE_ESTAMP(a, 11);
     float* sS = S.sdP;
-    for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
-        float v = 0.f;
-        if (k < m) {
-            for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
-            v += k == (int)threadIdx.x ? wb0 : a.Wb[k];
+    if (m > 8 * RAE_WAVE) {
+        for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
+            float v = 0.f;
+            if (k < m) {
+                for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
+                v += k == (int)threadIdx.x ? wb0 : a.Wb[k];
+            }
+            sS[k] = v;
         }
-        sS[k] = v;
+        __syncthreads();
     }
-    __syncthreads();
     RAE_ESTAMP(a, 12);
-    const int lane = threadIdx.x & 63;
     if (m <= 8 * RAE_WAVE) {
-        if (threadIdx.x < RAE_WAVE) {                      // wave 0: no block barriers
-            // the lane's scores in registers, one exp each (fast_softmax's form: P = e / sum e
-            // as e * (1 / sum e)); also sum_k P_k z_k (S.sred[41], the split forward's sz)
+        if (w0) {                                          // wave 0: no block barriers
+            // S = the slots' partial sums + Wb (slot order) and the softmax, the lane's scores in
+            // registers, one exp each (fast_softmax's form: P = e / sum e as e * (1 / sum e));
+            // also sum_k P_k z_k (S.sred[41], the split forward's sz)
             float sv[8], ev[8];
             float mx = -INFINITY;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int k = lane + RAE_WAVE * i;
-                sv[i] = k < m ? sS[k] : 0.f;
-                if (k < m) mx = fmaxf(mx, sv[i]);
+                float v = 0.f;
+                if (k < m) {
+                    for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
+                    v += wbk[i];
+                    mx = fmaxf(mx, v);
+                }
+                sv[i] = v;
             }
             mx = wave_max(mx);
             float se = 0.f;
@@ -1260,17 +1279,16 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     if (w < 2) {
         const float c0 = w == 0 ? dl : dr;
         float4 v = z4;
-        // branch-free over the lanes (lc: lanes past the row re-read column 0, not stored), so
-        // every readlane runs with the whole wave active -- a source lane outside EXEC has no
-        // defined value
-        vfma(v, c0, Rv[lc]);
+        // the coefficients broadcast (readlane) with the whole wave active -- a source lane
+        // outside EXEC has no defined value -- into scalars, then the row sum on the row's lanes
+        float ct[s];
 #pragma unroll
-        for (int t = 0; t < s; ++t) {
-            const float ct = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg),
-                                                                       (w == 0 ? 0 : 32) + t));
-            vfma(v, ct, Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lc]);
-        }
+        for (int t = 0; t < s; ++t)
+            ct[t] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dg), (w == 0 ? 0 : 32) + t));
         if (lv) {
+            vfma(v, c0, Rv[lane]);
+#pragma unroll
+            for (int t = 0; t < s; ++t) vfma(v, ct[t], Rv[(1 + (w == 0 ? 0 : s) + t) * RV + lane]);
             reinterpret_cast<float4*>(w == 0 ? S.sdw1 : S.sdw2)[lane] = v;
             rec_st(reinterpret_cast<float4*>(a.dwb + (int64_t)bg * a.dws + (w == 0 ? a.dw1o : a.dw2o)) + lane, v);
         }
