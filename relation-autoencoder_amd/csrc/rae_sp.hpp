@@ -350,15 +350,18 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     vzero(acc);
     const int lane = threadIdx.x & 63;
     const bool w0 = threadIdx.x < RAE_WAVE;
-    // the bias entries S adds (wave 0's for m <= 512, one per thread otherwise), loaded now so
-    // they are not a dependent round trip behind the W rows' barrier
-    float wbk[8];
+    // S = the slots' partial sums + Wb: for m <= 128 wave 0 forms its (<= 2 per lane) entries
+    // itself, right before the softmax (no barrier); larger m all threads, one entry each (wave
+    // 0 alone measured slower at m = 300).  The bias entries are loaded now, so they are not a
+    // dependent round trip behind the W rows' barrier.
+    const bool wS = m <= 2 * RAE_WAVE;
+    float wbk[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int k = lane + RAE_WAVE * i;
-        wbk[i] = (w0 && k < m && m <= 8 * RAE_WAVE) ? a.Wb[k] : 0.f;
+        wbk[i] = (wS && w0 && k < m) ? a.Wb[k] : 0.f;
     }
-    const float wb0 = (m > 8 * RAE_WAVE && threadIdx.x < m) ? a.Wb[threadIdx.x] : 0.f;
+    const float wb0 = (!wS && threadIdx.x < m) ? a.Wb[threadIdx.x] : 0.f;
     const bool vals = a.values != nullptr;
     bool issued = false;
     for (int pc = p0; pc < p1; pc += RAE_FBT) {
@@ -406,7 +409,7 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
     __syncthreads();
     RAE_ESTAMP(a, 11);
     float* sS = S.sdP;
-    if (m > 8 * RAE_WAVE) {
+    if (!wS) {
         for (int k = threadIdx.x; k < mp; k += RAE_FBT) {
             float v = 0.f;
             if (k < m) {
@@ -430,8 +433,12 @@ __device__ __forceinline__ void encoder_forward(const StepArgs& a, const D& Dm, 
                 const int k = lane + RAE_WAVE * i;
                 float v = 0.f;
                 if (k < m) {
-                    for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
-                    v += wbk[i];
+                    if (wS) {
+                        for (int sl = 0; sl < nslot; ++sl) v += S.spart[sl * m + k];
+                        v += wbk[i < 2 ? i : 0];
+                    } else {
+                        v = sS[k];
+                    }
                     mx = fmaxf(mx, v);
                 }
                 sv[i] = v;
