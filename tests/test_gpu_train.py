@@ -110,6 +110,11 @@ def _oracle_trajectory(decoder, data, seed, m, r, s, l, epochs, **hp):
     dict(N=300, d=2000, m=100, r=200, s=20, l=100, ntrue=10),   # headline K/r/s/l
     dict(N=240, d=500, m=30, r=100, s=10, l=60, ntrue=6),       # config 2 K/r/s
     dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5),          # non-multiple-of-4 (scalar path)
+    # the fused general path's other branches: s > 32 and r / 4 > 64 (the barrier-based
+    # coefficient / weighted-row blocks), m > 128 (S formed by all threads)
+    dict(N=300, d=400, m=8, r=16, s=36, l=40, ntrue=4),
+    dict(N=300, d=400, m=8, r=300, s=4, l=40, ntrue=4),
+    dict(N=300, d=800, m=200, r=16, s=4, l=40, ntrue=6),
     dict(N=400, d=300, m=8, r=16, s=4, l=50, ntrue=4, dec="rescal"),
     dict(N=210, d=700, m=7, r=13, s=3, l=70, ntrue=5, dec="rescal"),
     dict(N=200, d=2000, m=100, r=200, s=20, l=100, ntrue=10, dec="rescal", epochs=1),  # C5 shape
