@@ -72,8 +72,8 @@ __global__ __launch_bounds__(RAE_FBT) void k_sp_dec(StepArgs a) {
     sp_split_dec<V4>(a, step_batch(a), blockIdx.x / RAE_SPD_NP, blockIdx.x % RAE_SPD_NP, smem);
 }
 template <bool VEC>
-__global__ __launch_bounds__(RAE_BT) void k_sp_ctdw(StepArgs a) {
-    __shared__ __attribute__((aligned(16))) float red[RAE_BT * 4 + 16];
+__global__ __launch_bounds__(RAE_DW_BT) void k_sp_ctdw(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[RAE_DW_BT * 4 + 16];
     sp_split_ctdw<VEC>(a, blockIdx.x, red);
 }
 // SP dense partials (data parallel): this rank's dC1 / dC2 / dWb into its records, before the exchange
@@ -1174,8 +1174,8 @@ static void launch_fwd_sp(rae_plan* p, const StepArgs& a, hipStream_t st) {
         const dim3 gsd(RAE_SPD_NP * p->grid_fwd);          // a workgroup per (example, piece)
         if (p->v4) RAE_LAUNCH(p, k_sp_dec<true>, gsd, bt, p->smem_spd, st, a);
         else RAE_LAUNCH(p, k_sp_dec<false>, gsd, bt, p->smem_spd, st, a);
-        if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_BT), 0, st, a);
-        else RAE_LAUNCH(p, k_sp_ctdw<false>, gct, dim3(RAE_BT), 0, st, a);
+        if (a.r % 4 == 0) RAE_LAUNCH(p, k_sp_ctdw<true>, gct, dim3(RAE_DW_BT), 0, st, a);
+        else RAE_LAUNCH(p, k_sp_ctdw<false>, gct, dim3(RAE_DW_BT), 0, st, a);
         return;
     }
     const bool c3 = a.m == 100 && a.r == 200 && a.s == 20;

@@ -122,17 +122,24 @@ __device__ __forceinline__ float4 load4_guard(const float* p, int k, int n, bool
 __host__ __device__ inline int sp_cp_tasks(int l, int r) { return 2 * ((l + 15) / 16) * ((r + 15) / 16); }
 __host__ __device__ inline int sp_ctdw_tasks(int l, int m) { return ((l + 15) / 16) * ((m + 15) / 16); }
 
-// The two GEMMs: one 4-wave workgroup per 16 x 16 output tile; wave w takes the K chunks
-// c = w, w + 4, ... (16 deep each), RAE_SPG_U* chunks' loads issued before their MFMAs, and the
-// four waves' accumulators are combined in LDS in wave order (deterministic).
+// The two GEMMs: one workgroup per 16 x 16 output tile (k_sp_cp 4 waves, k_sp_ctdw RAE_DW_NW);
+// wave w takes the K chunks c = w, w + NW, ... (16 deep each), RAE_SPG_U* chunks' loads issued
+// before their MFMAs, and the waves' accumulators are combined in LDS in wave order
+// (deterministic; k_vrec repeats k_sp_cp's order).
 #ifndef RAE_SPG_UCP
 #define RAE_SPG_UCP 5   // k_sp_cp: 16-deep K chunks per wave per round (C4: m = 300, 19
                         // chunks over 4 waves -- all in one round)
 #endif
-#ifndef RAE_SPG_UDW
-#define RAE_SPG_UDW 5   // k_sp_ctdw (C4: 2r = 600, 38 chunks, two rounds; measured forward
-                        // 28.0 us at 5, 28.7 at 10 (one round), 28.8 at 4)
+#ifndef RAE_DW_NW
+#define RAE_DW_NW 8     // k_sp_ctdw: waves per tile workgroup (K split over them; C4 forward
+                        // 27.2 us at 4, 26.5 at 8, 26.9-27.3 at 16 -- profiles/r05_ab.txt)
 #endif
+#define RAE_DW_BT (RAE_DW_NW * RAE_WAVE)
+#ifndef RAE_SPG_UDW
+#define RAE_SPG_UDW 3   // k_sp_ctdw (C4: 2r = 600, 38 chunks over 8 waves, two rounds: 26.5 us,
+                        // as at 2; at 4 waves rounds of 5 measured 28.0, 10 28.7, 4 28.8)
+#endif
+template <int NW = RAE_NWAVE>
 __device__ __forceinline__ void sp_gemm_combine(rae_f32x4 acc, float* red, int lane, int w,
                                                 float out[4]) {
     float4* r4 = reinterpret_cast<float4*>(red);
@@ -141,7 +148,7 @@ __device__ __forceinline__ void sp_gemm_combine(rae_f32x4 acc, float* red, int l
     if (w == 0) {
         float4 t = r4[lane];
 #pragma unroll
-        for (int ww = 1; ww < RAE_NWAVE; ++ww) {
+        for (int ww = 1; ww < NW; ++ww) {
             const float4 u = r4[ww * 64 + lane];
             t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
         }
@@ -312,7 +319,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     const int b = bt * 16 + li, k = kt * 16 + li;
     const bool bv = b < l, kv = k < m;
     const int oS = sps_os(r4);
-    float* sdl = red + RAE_BT * 4;                        // [16]: sd of the tile's examples
+    float* sdl = red + RAE_DW_BT * 4;                     // [16]: sd of the tile's examples
     // this lane's GEMM row (example b): dl, dr from both sides' sums
     const float* spb = a.sps + (int64_t)(bv ? b : 0) * a.spss;
     const float* scb = spb + oS;
@@ -325,7 +332,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
         nv1 = sps_side(scb, 0, 2); nv2 = sps_side(scb, 1, 2);
     }
     // the tile's stores of dw1, dw2, G1: pair (example eo, column ii) per thread
-    const int pr = threadIdx.x, eo = pr >> 4, ii = pr & 15;
+    const int pr = threadIdx.x & 255, eo = pr >> 4, ii = pr & 15;   // waves >= 4 repeat 0-3's
     const int bo_s = bt * 16 + eo;
     const bool sv = bo_s < l;
     const int bs = sv ? bo_s : 0;
@@ -358,11 +365,11 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     }
     rae_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int nci = (r + 15) / 16, nch = 2 * nci;
-    for (int c0 = w; c0 < nch; c0 += RAE_NWAVE * RAE_SPG_UDW) {
+    for (int c0 = w; c0 < nch; c0 += RAE_DW_NW * RAE_SPG_UDW) {
         float4 x[RAE_SPG_UDW], y[RAE_SPG_UDW];
 #pragma unroll
         for (int u = 0; u < RAE_SPG_UDW; ++u) {
-            const int c = c0 + u * RAE_NWAVE;
+            const int c = c0 + u * RAE_DW_NW;
             const bool cv = c < nch;
             const int which = c >= nci, i = (c - which * nci) * 16 + 4 * g;
             const float* Cm = which ? a.C2 : a.C1;
@@ -389,18 +396,19 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
         const float dl = s_du1 + s_du2 + s_sdg2, dr = s_du1 + s_du2 + s_sdg1;
         float* dwr = a.dwb + (int64_t)(a.rank * l + bs) * a.dws;
         float* rec = a.ex + (int64_t)(a.rank * l + bs) * a.lay.rec;
-        if (iv0) {
+        const bool st = threadIdx.x < 256;
+        if (iv0 && st) {
             dwr[a.dw1o + is0] = fmaf(dl, sa0, sn10);
             dwr[a.dw2o + is0] = fmaf(dr, sa0, sn20);
             if (!a.lay.wire) rec[a.lay.oG1 + is0] = fmaf(dl, sv10, dr * sv20);
         }
-        for (int is = is0 + 16 * nkt; sv && is < r; is += 16 * nkt) {    // r > 16 nkt only
+        for (int is = is0 + 16 * nkt; st && sv && is < r; is += 16 * nkt) {    // r > 16 nkt only
             const float ae = sps_s[sps_oa(r4) + is];
             dwr[a.dw1o + is] = fmaf(dl, ae, sps_rowsum(sps_s, 0, is, r4));
             dwr[a.dw2o + is] = fmaf(dr, ae, sps_rowsum(sps_s, 1, is, r4));
             if (!a.lay.wire) rec[a.lay.oG1 + is] = fmaf(dl, vrow[a.vV1 + is], dr * vrow[a.vV2 + is]);
         }
-        if (lossl) {
+        if (lossl && st) {
             rec[a.lay.oloss] = lbase + sls;
             if (a.lay.wire) {                             // k_vrec rebuilds G1 from (dl, dr)
                 rec[a.lay.oAux + 0] = dl;
@@ -410,7 +418,7 @@ __device__ void sp_split_ctdw(const StepArgs& a, int task, float* red) {
     }
     if (w == 0 && g == 0) sdl[li] = fmaf(dlb, lft, nv1) + fmaf(drb, rgt, nv2);
     float o[4];
-    sp_gemm_combine(acc, red, lane, w, o);                // its barrier also publishes sdl
+    sp_gemm_combine<RAE_DW_NW>(acc, red, lane, w, o);     // its barrier also publishes sdl
     if (w != 0) return;
     // epilogue: dS_bk = P_bk ((dP_bk - sd_b) + ce (z_bk - sz_b))   (softmax_backward's centred
     // form)
