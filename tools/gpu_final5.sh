@@ -43,7 +43,10 @@ print('pmc $c', {k: (round(v['traffic_bytes']/1e6, 2) if isinstance(v, dict) and
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
         GRBM_GUI_ACTIVE -f csv -d $O/mfma -o run -- python3 $R/bench.py --config c5 --steps 64 --warmup 16 \
         --no-cpu-baseline --no-label-pass --kernel-iters 32 > $O/mfma.log 2>&1) || { echo mfma failed; tail -20 $O/mfma.log; exit 1; }
-      python3 tools/pmc_mfma.py $O/mfma --out $O/r05_c5_pmc_mfma.json > $O/mfma_post.log 2>&1 || { echo mfma post failed; tail $O/mfma_post.log; exit 1; }
+      # mfma_util_span needs the kernels' average durations: this tag's stats:c5 pass if it ran
+      # first, else the committed summary
+      ST=$O/r05_c5_kernel_stats.csv; [ -f $ST ] || ST=profiles/r05_c5_kernel_stats.csv
+      python3 tools/pmc_mfma.py $O/mfma --stats $ST --out $O/r05_c5_pmc_mfma.json > $O/mfma_post.log 2>&1 || { echo mfma post failed; tail $O/mfma_post.log; exit 1; }
       python3 -c "
 import json; d=json.load(open('$O/r05_c5_pmc_mfma.json'))['per_kernel']
 for k, v in d.items():
