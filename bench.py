@@ -265,6 +265,9 @@ def main():
                     help="partitioned update, N > 1: RCCL collectives between the step launches, or "
                          "the kernels' own stores into the peers' IPC-mapped buffers (include/rae.h "
                          "RAE_XCHG_P2P)")
+    ap.add_argument("--p2p-cross-device", action="store_true",
+                    help="--dp-xchg p2p with ranks on different GPUs (verified on ranks sharing "
+                         "one GPU only; refused without this flag)")
     args = ap.parse_args()
     if args.dp_xchg == "p2p":
         args.dp_update = "partitioned"
@@ -295,7 +298,8 @@ def main():
                              graph_chunk=args.graph_chunk, mfma_bf16=cfg.get("bf16", False),
                              dp_update=args.dp_update,
                              kernel_forms=dict(kv.split("=", 1) for kv in args.kernel_form),
-                             index_overlap=not args.no_index_overlap)
+                             index_overlap=not args.no_index_overlap,
+                             p2p_cross_device=args.p2p_cross_device)
     ind.compile_function()
     eng = ind.engine
     # per-epoch negatives: the reference's RandomState stream, CDF search on the device
@@ -344,7 +348,7 @@ def main():
         npref = max(0, min(K, nb - W - K))
     # no run follows the timed one on this cursor: its last graph skips the cursor advance
     eng.run(W, K, index=not prebuilt, last_advance=False,
-            prefetch=None if not prebuilt else npref > 0)
+            prefetch=None if not prebuilt else npref > 0, sync_peers=False)
     t_host = time.perf_counter() - t0          # host time to queue the timed region's work
     torch.cuda.synchronize()
     rdist.barrier()

@@ -42,10 +42,12 @@ typedef struct ihipStream_t* rae_stream_t;   /* == hipStream_t */
 #define RAE_E_INVALID (-1)     /* bad argument / unsupported configuration           */
 #define RAE_E_HIP (-2)         /* HIP runtime error                                  */
 #define RAE_E_OVERFLOW (-3)    /* a per-step row-index partition overflowed its LDS  */
-#define RAE_E_STATE (-4)       /* call sequence error                                */
-/* device error word bits (rae_check): 1 / 2 an A / W row-index partition overflowed its LDS
- * sort, 4 a batch exceeded the index's record capacity, 8 / 16 a data-parallel row list
- * overflowed, 64 a peer-to-peer wait timed out (a peer stopped signalling)                 */
+#define RAE_E_STATE (-4)       /* call sequence error; a peer-to-peer wait timed out */
+/* device error word bits (rae_check; rae_last_error names each set bit): 1 / 2 an A / W
+ * row-index partition overflowed its LDS sort, 4 a batch exceeded the index's record capacity,
+ * 8 a data-parallel row list overflowed while being built, 16 a row list is longer than the
+ * exchange's row capacity (RAE_E_OVERFLOW for these); 64 a peer-to-peer wait timed out -- a
+ * peer stopped signalling (RAE_E_STATE)                                                      */
 
 /* decoder type: learning/models/decoders/Decoder.py:84-93 ('sp', 'rescal', 'rescal+sp') */
 #define RAE_DEC_SP 0
@@ -262,11 +264,15 @@ int rae_ipc_export(const void* dev_ptr, void* handle_out, int64_t* offset_out);
 /* map another process's allocation (its base address; add the exported offset)            */
 int rae_ipc_open(const void* handle, void** base_out);
 int rae_ipc_close(void* base);
-/* the plan's signal counters (device; export them to the peers)                            */
+/* the plan's signal counters (device, uncached; export them to the peers)                  */
 void* rae_p2p_signals(rae_plan* plan);
 /* peer `peer`'s buffers as this process maps them                                          */
 int rae_set_peer(rae_plan* plan, int32_t peer, float* exchange_dev, float* W_dev, float* A_dev,
                  float* Ab_dev, void* signals_dev);
+/* how long one wait kernel may spin for a peer's signal before it sets error bit 64 and
+ * gives up (default 5 s; a driver that does host work between steps -- per-batch evaluation
+ * -- raises it or puts a host barrier in front of the next step)                          */
+int rae_set_p2p_timeout(rae_plan* plan, double seconds);
 
 /* Kernel timing (bench / profiling; no reference counterpart).  Arms the NEXT
  * rae_step_forward or rae_step_update call on this plan: its kernels are launched with

@@ -972,7 +972,10 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     }
     *p->h_err = 0;
     if (c.dp_xchg == RAE_XCHG_P2P) {
-        e = hipMalloc(reinterpret_cast<void**>(&p->d_sig), 4ull * 2 * c.world_size);
+        // the peers add to these words over xGMI and this rank polls them: uncached (no L2
+        // line of them can go stale; rae_p2p.hpp "Visibility across GPUs")
+        e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->d_sig), 4ull * 2 * c.world_size,
+                                  hipDeviceMallocUncached);
         if (e == hipSuccess) e = hipMemset(p->d_sig, 0, 4ull * 2 * c.world_size);
         if (e != hipSuccess) {
             (void)hipFree(p->ws);
@@ -1098,6 +1101,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
                                   (int)(4 * RAE_DPL_KEYS + 4 * 32));
     }
     a.sig = p->d_sig;
+    a.p2p_timeout = RAE_P2P_TIMEOUT_DEFAULT;
     if (a.sig) {                 // this rank's own entry of the peer table
         const PeerBufs own{a.ex, a.W, a.A, a.Ab, a.sig};
         if (hipMemcpy(a.peers + c.rank, &own, sizeof(own), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1545,6 +1549,13 @@ extern "C" int rae_set_peer(rae_plan* p, int32_t peer, float* exchange, float* W
     p->peers_set = p->peers_mask == (((1 << p->args.G) - 1) & ~(1 << p->args.rank));
     return RAE_OK;
 }
+extern "C" int rae_set_p2p_timeout(rae_plan* p, double seconds) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (p->args.xchg != RAE_XCHG_P2P) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
+    if (!(seconds > 0.0) || seconds > 3600.0) return fail(RAE_E_INVALID, "timeout must be in (0, 3600] s");
+    p->args.p2p_timeout = (unsigned long long)(seconds * 1e8);   // s_memrealtime: 100 MHz
+    return RAE_OK;
+}
 
 extern "C" int rae_time_next(rae_plan* p, void* start, void* stop) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
@@ -1602,12 +1613,23 @@ extern "C" int rae_debug_grid(rae_plan* p, int* out) {
 }
 #endif
 
+// the device error word, bit by bit (rae.h): a peer-to-peer wait timeout is a state error (a
+// peer stopped signalling), everything else a capacity overflow
 static int err_flags(int e) {
-    if (e) return fail(RAE_E_OVERFLOW, std::string(e & 8 ? "a data-parallel row list overflowed "
-                                                         "its capacity; " : "") +
-                                           "row-index partition overflow (flags=" +
-                                           std::to_string(e) + ")");
-    return RAE_OK;
+    if (!e) return RAE_OK;
+    static const struct { int bit; const char* what; } bits[] = {
+        {1, "an entity-row index partition overflowed its LDS sort"},
+        {2, "a feature-row index partition overflowed its LDS sort"},
+        {4, "a batch exceeded the row index's record capacity"},
+        {8, "a data-parallel row list overflowed while being built"},
+        {16, "a data-parallel row list is longer than the exchange's row capacity"},
+        {64, "a peer-to-peer wait timed out (a peer stopped signalling)"},
+    };
+    std::string msg;
+    for (const auto& b : bits)
+        if (e & b.bit) msg += (msg.empty() ? "" : "; ") + std::string(b.what);
+    msg += " (device error flags=" + std::to_string(e) + ")";
+    return fail(e & 64 ? RAE_E_STATE : RAE_E_OVERFLOW, msg);
 }
 extern "C" int rae_check(rae_plan* p) {
     if (!p) return fail(RAE_E_INVALID, "null plan");

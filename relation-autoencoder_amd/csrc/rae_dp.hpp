@@ -30,6 +30,7 @@
 namespace rae {
 
 #define RAE_DPL_KEYS 16384      // uint32 keys per LDS sort pass (64 KiB)
+#define RAE_DPL_HMAX 1024       // hash passes of one list before an overflow is an error
 
 // list storage of one batch slot: [dir 2][peer G][A list LA | W list LW] ints; counts
 // [slot][dir][peer][table] ints
@@ -65,9 +66,18 @@ __device__ void build_dp_list(const StepArgs& a, int64_t g, int64_t slot, int di
     const int NJ = 2 + 2 * a.s;
     const int P0 = tab ? a.indptr[ex0] : 0;
     const int ncand = tab ? a.indptr[ex0 + a.l] - P0 : a.l * NJ;
-    // hash passes (row / G) % H: sized from the candidates rank y keeps (~1 / G of them, twice
-    // that for the Zipf skew) -- one pass of the scan and sort where ncand / RAE_DPL_KEYS passes
-    // had each re-scanned every candidate
+    // candidate idx: a feature id of the rank's CSR rows, or entity slot j of example b
+    // (j-major: coalesced columns)
+    auto cand = [&](int idx) -> int {
+        if (tab) return a.indices[P0 + idx];
+        const int j = idx / a.l, b = idx - j * a.l;
+        const int64_t ex = ex0 + b;
+        const int64_t col = a.neg_mode ? ex : (int64_t)x * a.l + b;
+        if (j == 0) return a.args1[ex];
+        if (j == 1) return a.args2[ex];
+        if (j < 2 + a.s) return a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
+        return a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
+    };
     // the rows rank y owns are y + G q, q < nq: when a bit per q fits the LDS, the list is a
     // bitmap -- one atomicOr per candidate, then the set bits in ascending q by a block scan of
     // the words' popcounts: ascending rows, the sort path's order, without the sort (which was
@@ -78,18 +88,7 @@ __device__ void build_dp_list(const StepArgs& a, int64_t g, int64_t slot, int di
         for (int i = tid; i < nw; i += BT) keys[i] = 0u;
         __syncthreads();
         for (int idx = tid; idx < ncand; idx += BT) {
-            int row;
-            if (tab) {
-                row = a.indices[P0 + idx];
-            } else {
-                const int j = idx / a.l, b = idx - j * a.l;        // j-major: coalesced columns
-                const int64_t ex = ex0 + b;
-                const int64_t col = a.neg_mode ? ex : (int64_t)x * a.l + b;
-                if (j == 0) row = a.args1[ex];
-                else if (j == 1) row = a.args2[ex];
-                else if (j < 2 + a.s) row = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
-                else row = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
-            }
+            const int row = cand(idx);
             if (row % G == y) {
                 const int q = row / G;
                 atomicOr(&keys[q >> 5], 1u << (q & 31));
@@ -117,64 +116,73 @@ __device__ void build_dp_list(const StepArgs& a, int64_t g, int64_t slot, int di
         }
         return;
     }
-    const int H = (2 * ((ncand + G - 1) / G) + RAE_DPL_KEYS - 1) / RAE_DPL_KEYS;
+    // larger vocabularies: hash passes (row / G) % H, each sorting its owned candidates in
+    // LDS.  H is sized from the owned candidates counted first (duplicates included: a pass
+    // holds every occurrence), twice over for the hash's imbalance; a pass that still
+    // overflows (a Zipf-heavy row's occurrences in one bucket) restarts the list with H doubled
+    //  -- an overflow is an error only beyond RAE_DPL_HMAX passes
+    int own = 0;
+    for (int idx = tid; idx < ncand; idx += BT) own += cand(idx) % G == y;
+    int nown;
+    (void)block_int_scan<BT>(own, sint + 1, &nown);
+    int H = max(1, (2 * nown + RAE_DPL_KEYS - 1) / RAE_DPL_KEYS);
     int total = 0;
-    for (int h = 0; h < (H > 0 ? H : 1); ++h) {
-        if (tid == 0) sint[0] = 0;
-        __syncthreads();
-        for (int idx = tid; idx < ncand; idx += BT) {
-            int row;
-            if (tab) {
-                row = a.indices[P0 + idx];
-            } else {
-                const int j = idx / a.l, b = idx - j * a.l;        // j-major: coalesced columns
-                const int64_t ex = ex0 + b;
-                const int64_t col = a.neg_mode ? ex : (int64_t)x * a.l + b;
-                if (j == 0) row = a.args1[ex];
-                else if (j == 1) row = a.args2[ex];
-                else if (j < 2 + a.s) row = a.neg1[(int64_t)(j - 2) * a.neg_stride + col];
-                else row = a.neg2[(int64_t)(j - 2 - a.s) * a.neg_stride + col];
+    for (;;) {
+        bool over = false;
+        total = 0;
+        for (int h = 0; h < H; ++h) {
+            if (tid == 0) sint[0] = 0;
+            __syncthreads();
+            for (int idx = tid; idx < ncand; idx += BT) {
+                const int row = cand(idx);
+                if (row % G == y && (H <= 1 || (row / G) % H == h)) {
+                    const int sl = atomicAdd(&sint[0], 1);
+                    if (sl < RAE_DPL_KEYS) keys[sl] = (unsigned)row;
+                }
             }
-            if (row % G == y && (H <= 1 || (row / G) % H == h)) {
-                const int sl = atomicAdd(&sint[0], 1);
-                if (sl < RAE_DPL_KEYS) keys[sl] = (unsigned)row;
+            __syncthreads();
+            const int cnt = sint[0];
+            __syncthreads();                      // every thread has read cnt before a reset
+            if (cnt > RAE_DPL_KEYS) {
+                over = true;
+                break;
             }
+            int n2 = 1;
+            while (n2 < cnt) n2 <<= 1;
+            for (int i = cnt + tid; i < n2; i += BT) keys[i] = 0xffffffffu;
+            __syncthreads();
+            for (int k = 2; k <= n2; k <<= 1) {                      // bitonic sort, ascending
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < n2; i += BT) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned u = keys[i], v = keys[ixj];
+                            if ((u > v) == ((i & k) == 0)) {
+                                keys[i] = v;
+                                keys[ixj] = u;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // distinct rows in order
+            for (int i0 = 0; i0 < cnt; i0 += BT) {
+                const int i = i0 + tid;
+                const bool head = i < cnt && (i == 0 || keys[i - 1] != keys[i]);
+                int tot;
+                const int pos = total + block_flag_scan<BT>(head, sint + 1, &tot);
+                if (head && pos < cap) out[pos] = (int32_t)keys[i];
+                total += tot;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        const int cnt = sint[0];
-        if (cnt > RAE_DPL_KEYS) {
+        if (!over) break;
+        H *= 2;
+        if (H > RAE_DPL_HMAX) {
             if (tid == 0) atomicOr(a.err, 8);
             return;
         }
-        int n2 = 1;
-        while (n2 < cnt) n2 <<= 1;
-        for (int i = cnt + tid; i < n2; i += BT) keys[i] = 0xffffffffu;
-        __syncthreads();
-        for (int k = 2; k <= n2; k <<= 1) {                      // bitonic sort, ascending
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < n2; i += BT) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const unsigned u = keys[i], v = keys[ixj];
-                        if ((u > v) == ((i & k) == 0)) {
-                            keys[i] = v;
-                            keys[ixj] = u;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        // distinct rows in order
-        for (int i0 = 0; i0 < cnt; i0 += BT) {
-            const int i = i0 + tid;
-            const bool head = i < cnt && (i == 0 || keys[i - 1] != keys[i]);
-            int tot;
-            const int pos = total + block_flag_scan<BT>(head, sint + 1, &tot);
-            if (head && pos < cap) out[pos] = (int32_t)keys[i];
-            total += tot;
-        }
-        __syncthreads();
     }
     if (tid == 0) {
         *cnt_out = total;

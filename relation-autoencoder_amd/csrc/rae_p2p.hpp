@@ -14,14 +14,28 @@
 //   k_p2p_recs   its l records into every peer's exchange buffer, at the same rows
 //   k_p2p_wait   (records): until every peer's records of batch b are here
 //   update(b)    the owned rows, as before
-// Signalling: after a push kernel (its stores released at the kernel boundary) a one-wave
-// signal kernel fences at system scope and adds one to the peer's signal word (kind, this rank)
-// with a system-scope release -- a counter that grows by one every step (fences per workgroup
-// inside the pushes cost an L2 write-back each: 55-81 us per step in the loopback model).  The waiting kernel (one wave: lane p watches peer p) spins
-// on acquire loads until each counter reaches its expected value (kept in this rank's private
-// words, advanced by the wait kernel itself, so graph replays stay in step), with a bounded spin:
-// after RAE_P2P_TIMEOUT it sets error bit 64 and returns (the host sees it at rae_check) rather
-// than hold the GPU.
+// Signalling: after a push kernel a one-wave signal kernel fences at system scope and adds one
+// to the peer's signal word (kind, this rank) with a system-scope release -- a counter that
+// grows by one every step (fences per workgroup inside the pushes cost an L2 write-back each:
+// 55-81 us per step in the loopback model).  The waiting kernel (one wave: lane p watches peer
+// p) spins on relaxed system-scope loads until each counter reaches its expected value (kept in
+// this rank's private words, advanced by the wait kernel itself, so graph replays stay in
+// step), with a bounded spin: after StepArgs::p2p_timeout (rae_set_p2p_timeout; 5 s by default)
+// it sets error bit 64 and returns (the host sees it at rae_check) rather than hold the GPU.
+// Visibility across GPUs ("peer-to-peer visibility"), each side made explicit:
+//  * producer: every push store is a system-scope write-through (`global_store ... sc0 sc1`,
+//    store_sys below) and each pushing wave waits for its stores to complete (vmcnt(0)) before
+//    it ends -- no pushed byte can sit dirty in one of this GPU's eight L2s (a peer's memory is
+//    mapped non-coherent here, and the signal kernel's single-wave fence writes back one XCD's
+//    L2 only), so the bytes are in the peer's memory before the kernel boundary, and the
+//    signal add follows that boundary;
+//  * signal words: allocated uncached (hipDeviceMallocUncached), so neither the polls nor the
+//    peers' atomic adds go through an L2 line that could be stale;
+//  * consumer: the pushed rows / records land in this rank's own coarse-grained memory; the
+//    peers' stores reach it through its data fabric like another XCD's write-backs do, and the
+//    kernels that read them start after the wait kernel's acquire and their own dispatch
+//    acquire (L1 invalidated) -- the same hand-off the MI355X guide measures cross-XCD with an
+//    L1 invalidate alone (MI355X_MICROARCH.md:161-174).  Untested across physical GPUs.
 // Hazards (all ranks run the same step sequence): a peer's replica rows and exchange rows are
 // overwritten only after that peer has consumed them -- owner k's row stores of batch b follow
 // k's update of b - 1, which needed peer p's records of b - 1, which p pushed after its forward
@@ -36,13 +50,23 @@
 
 namespace rae {
 
-#ifndef RAE_P2P_TIMEOUT
-#define RAE_P2P_TIMEOUT 500000000ull   // s_memrealtime ticks (100 MHz): 5 s
-#endif
+#define RAE_P2P_TIMEOUT_DEFAULT 500000000ull   // s_memrealtime ticks (100 MHz): 5 s
 
-// k_p2p_signal (one wave, after a push kernel): the push's stores were released at the kernel
-// boundary (on gfx950 an agent-scope release writes the L2s back, every XCD's); this fences at
-// system scope once more and counts one signal into every peer's word (kind, rank)
+// system-scope write-through stores into a peer's memory (sc0 sc1: not held in this GPU's L2);
+// the caller's wave waits for them with p2p_stores_done() before it ends
+__device__ __forceinline__ void store_sys(float4* p, float4 v) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ void store_sys(float* p, float v) {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void p2p_stores_done() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
+
+// k_p2p_signal (one wave, after a push kernel): the push's stores completed at system scope
+// before its waves ended (store_sys + vmcnt(0)); this fences at system scope once more and
+// counts one signal into every peer's (uncached) word (kind, rank)
 __device__ void p2p_signal(const StepArgs& a, int kind) {
     __threadfence_system();
     if (threadIdx.x < a.G && threadIdx.x != a.rank) {
@@ -59,7 +83,8 @@ __device__ void p2p_push_records(const StepArgs& a) {
     if (i >= n4) return;
     const float4 v = reinterpret_cast<const float4*>(a.ex)[o4 + i];
     for (int p = 0; p < a.G; ++p)
-        if (p != a.rank) reinterpret_cast<float4*>(a.peers[p].ex)[o4 + i] = v;
+        if (p != a.rank) store_sys(reinterpret_cast<float4*>(a.peers[p].ex) + o4 + i, v);
+    p2p_stores_done();
 }
 
 // k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
@@ -88,9 +113,10 @@ __device__ void p2p_push_rows(const StepArgs& a) {
     if (lane < w4) v0 = s[lane];
     if (lane + 64 < w4) v1 = s[lane + 64];
     const float ab = (!tab && lane == 0) ? a.Ab[row] : 0.f;
-    if (lane < w4) d[lane] = v0;
-    if (lane + 64 < w4) d[lane + 64] = v1;
-    if (!tab && lane == 0) a.peers[p].Ab[row] = ab;
+    if (lane < w4) store_sys(d + lane, v0);
+    if (lane + 64 < w4) store_sys(d + lane + 64, v1);
+    if (!tab && lane == 0) store_sys(a.peers[p].Ab + row, ab);
+    p2p_stores_done();
 }
 
 // k_p2p_wait: lane p waits for peer p's `per` signals of this step (kind 0 records, 1 rows):
@@ -105,7 +131,7 @@ __device__ void p2p_wait(const StepArgs& a, int kind, unsigned per) {
     // a wait that already timed out this run: do not wait again (fail fast; rae_check raises)
     const bool dead = (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 64) != 0;
     while (!dead && (int)(__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > RAE_P2P_TIMEOUT) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.p2p_timeout) {
             atomicOr(a.err, 64);
             break;
         }

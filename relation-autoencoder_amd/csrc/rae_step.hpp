@@ -214,8 +214,9 @@ struct StepArgs {
     // rank's signal counters (written by the peers) and its expected counts (private)
     int xchg;
     PeerBufs* peers;
-    unsigned* sig;
+    unsigned* sig;       // uncached allocation (rae.hip: hipDeviceMallocUncached)
     unsigned* p2p_expect;
+    unsigned long long p2p_timeout;   // s_memrealtime ticks (100 MHz) a wait may spin
     // private rows: rows a single record of the global batch references (rae.h RAE_PRIV_AUTO;
     // single-rank SP plans), updated per example by the update launch's leading workgroups;
     // pmask per slot and example = (entity-slot bits j < 32, j >= 32, feature-position bits,

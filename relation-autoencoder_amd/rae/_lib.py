@@ -77,6 +77,7 @@ EXPORTS = (
     "rae_dp_block_floats", "rae_set_dp_buffers", "rae_dp_list_max", "rae_dp_pack",
     "rae_dp_unpack", "rae_dp_pack_at", "rae_dp_unpack_at",
     "rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_p2p_signals", "rae_set_peer",
+    "rae_set_p2p_timeout",
 )
 RAE_IPC_HANDLE_BYTES = 64
 
@@ -171,7 +172,9 @@ def load(path: str | None = None):
     lib.rae_p2p_signals.argtypes = [_P]
     lib.rae_p2p_signals.restype = _P
     lib.rae_set_peer.argtypes = [_P, C.c_int32, _P, _P, _P, _P, _P]
-    for fn in ("rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_set_peer"):
+    lib.rae_set_p2p_timeout.argtypes = [_P, C.c_double]
+    for fn in ("rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_set_peer",
+               "rae_set_p2p_timeout"):
         getattr(lib, fn).restype = C.c_int
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]

@@ -101,6 +101,11 @@ class Exchange:
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    def barrier(self):
+        """Host barrier of the ranks (the peer-to-peer exchange's run starts: no rank queues a
+        step whose wait kernel would spin while a peer is still in host code)."""
+        dist.barrier(group=self.group)
+
     def max_int(self, v: int) -> int:
         dev = torch.device("cuda", torch.cuda.current_device()) if \
             dist.get_backend(self.group) == "nccl" else torch.device("cpu")

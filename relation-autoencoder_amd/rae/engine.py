@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import socket
 
 import numpy as np
 import torch
@@ -46,6 +47,18 @@ def _upload_graph(g, stream):
         pass
 
 
+def check_p2p_devices(identities, cross_device: bool):
+    """The peer-to-peer exchange's device guard: ranks whose GPUs differ are
+    refused unless cross_device -- the kernels' stores into a peer GPU's memory have run on
+    ranks sharing one GPU only (rae_p2p.hpp "Visibility across GPUs")."""
+    devs = sorted(set(identities))
+    if len(devs) > 1 and not cross_device:
+        raise ValueError(
+            f"dp_xchg='p2p' across {len(devs)} GPUs: the peer-to-peer exchange is verified on "
+            "ranks sharing one GPU only; pass p2p_cross_device=True to run it across GPUs (or "
+            "use dp_xchg='collective', the default)")
+
+
 class DeviceSplit:
     """One split's CSR + entity ids in HBM (int32; values kept only if not all 1.0)."""
 
@@ -69,7 +82,8 @@ class TrainEngine:
     def __init__(self, model, optimizer, train_split, *, learning_rate, lambda1=0.0,
                  lambda2=0.0, world_size=1, rank=0, exchange=None, graph_chunk=64,
                  index_window=0, device=None, mfma_bf16=False, kernel_forms=None,
-                 graph_absolute=False, dp_update="replicated", index_overlap=True):
+                 graph_absolute=False, dp_update="replicated", index_overlap=True,
+                 p2p_cross_device=False, p2p_timeout=5.0):
         self.lib = _lib.load()
         self.model = model
         self.device = device if device is not None else model.params[0].device
@@ -128,6 +142,10 @@ class TrainEngine:
         if self.kernel_forms.get("dp_xchg") == "p2p" and self.kernel_forms["dp_update"] != "partitioned":
             raise ValueError("the peer-to-peer exchange runs the partitioned update")
         self._ipc_bases = {}         # handle bytes -> this process's mapping of a peer allocation
+        # ranks on different GPUs: the kernels' xGMI stores into a peer's memory (rae_p2p.hpp
+        # "Visibility across GPUs") have run on ranks sharing one GPU only -- opt-in
+        self._p2p_cross_device = bool(p2p_cross_device)
+        self._p2p_timeout = float(p2p_timeout)
         for key, val in self.kernel_forms.items():
             if key not in _lib.KERNEL_FORMS or val not in _lib.KERNEL_FORMS[key]:
                 raise ValueError(f"unknown kernel form {key}={val!r}")
@@ -224,18 +242,30 @@ class TrainEngine:
             base = self._ipc_bases[handle] = int(b.value)
         return base + offset
 
+    def _device_identity(self):
+        try:
+            return str(torch.cuda.get_device_properties(self.device).uuid)
+        except (AttributeError, RuntimeError):
+            return f"{socket.gethostname()}:{self.device.index}"
+
     def _p2p_setup(self):
         """Trade IPC handles of this rank's exchange buffer, W, A, Ab and signal counters with
         every peer (a collective over the ranks' process group, once) and hand the peers'
-        mappings to the plan (rae_set_peer).  Tensors sharing one allocation map it once."""
+        mappings to the plan (rae_set_peer).  Tensors sharing one allocation map it once.
+        Ranks on different GPUs are refused unless p2p_cross_device=True (the
+        cross-GPU stores have not run on hardware)."""
         named = self._named
         sig = self.lib.rae_p2p_signals(self.plan)
         mine = {"ex": self._ipc_export(self.exchange_buf.data_ptr()),
                 "W": self._ipc_export(named["W"].data_ptr()),
                 "A": self._ipc_export(named["A"].data_ptr()),
                 "Ab": self._ipc_export(named["Ab"].data_ptr()),
-                "sig": self._ipc_export(int(sig))}
+                "sig": self._ipc_export(int(sig)),
+                "dev": self._device_identity()}
         everyone = self.exchange.all_gather_object(mine)
+        check_p2p_devices([e["dev"] for e in everyone], self._p2p_cross_device)
+        _lib.check(self.lib.rae_set_p2p_timeout(self.plan, C.c_double(self._p2p_timeout)),
+                   "rae_set_p2p_timeout")
         for p, e in enumerate(everyone):
             if p == self.rank:
                 continue
@@ -576,7 +606,7 @@ class TrainEngine:
             self._dp_caps_check()
 
     def run(self, first_batch: int, count: int, graph: bool = True, index: bool = True,
-            last_advance: bool = True, prefetch: bool | None = None):
+            last_advance: bool = True, prefetch: bool | None = None, sync_peers: bool = True):
         """Run ``count`` consecutive global batches starting at ``first_batch`` on the epoch
         negatives; costs land in self.costs[first_batch:first_batch+count].  The row index
         of each window of batches is ready before the window's steps (index=False: the caller
@@ -585,10 +615,17 @@ class TrainEngine:
         next window, or as many batches as the window after the run's last -- is built on the
         side stream, queued in front of the window's steps so it runs beside them.  With
         graph, every step runs inside a replayed HIP graph: graph_chunk-step graphs and one
-        graph per window remainder (last_advance: see _cursor_replays)."""
+        graph per window remainder (last_advance: see _cursor_replays).  sync_peers (the
+        peer-to-peer exchange only): a host barrier of the ranks first -- a caller that has
+        just met its peers (bench.py's timed region) may skip it."""
         self._ensure_epoch_mode()
         if self._dp:
             self._stale.update(("params", "acc"))
+        if self._p2p and sync_peers:
+            # a peer may have spent any time in host code since its last step (per-batch
+            # evaluation, checkpoints): meet here so no wait kernel of this run starts its
+            # bounded spin (rae_set_p2p_timeout) while a peer is still away (ADVICE r5)
+            self.exchange.barrier()
         pre = (index if prefetch is None else prefetch) and self.index_overlap
         replays = self._cursor_replays(first_batch, count, last_advance)
         wins = self.windows(first_batch, count)

@@ -55,7 +55,7 @@ class ReconstructInducer:
                  frequent_eval, alpha, *, device=None, world_size=1, rank=0, exchange=None,
                  graph_chunk=64, neg_sampler="device", neg_seed=0, mfma_bf16=False,
                  kernel_forms=None, dp_update="replicated", index_window=0,
-                 index_overlap=True):
+                 index_overlap=True, p2p_cross_device=False, p2p_timeout=5.0):
         self.data = data
         self.goldStandard = gold_standard
         self.rng = rng
@@ -88,6 +88,10 @@ class ReconstructInducer:
         self.index_window = int(index_window)          # engine.TrainEngine row-index ring
         self.index_overlap = bool(index_overlap)       # next window's index beside the steps
         self.dp_update = dp_update         # "replicated" | "partitioned" (rae/dist.py)
+        # peer-to-peer exchange (kernel_forms dp_xchg="p2p"): ranks on different GPUs only
+        # when asked for (engine.TrainEngine._p2p_setup); a wait's bound in seconds
+        self.p2p_cross_device = bool(p2p_cross_device)
+        self.p2p_timeout = float(p2p_timeout)
         self.negativeSampler = NegativeExampleGenerator(rng, data.negSamplingCum)   # :85
         self.modelID = (f"{decoder_model}_{model_name}_maxepoch{nb_epochs}_lr{learning_rate}"
                         f"_embedsize{embed_size}_l1{lambda1}_l2{lambda2}_opt{optimization}"
@@ -152,7 +156,9 @@ class ReconstructInducer:
                                   graph_chunk=self.graph_chunk, device=self.device,
                                   mfma_bf16=self.mfma_bf16, kernel_forms=self.kernel_forms,
                                   dp_update=self.dp_update, index_window=self.index_window,
-                                  index_overlap=self.index_overlap)
+                                  index_overlap=self.index_overlap,
+                                  p2p_cross_device=self.p2p_cross_device,
+                                  p2p_timeout=self.p2p_timeout)
         self.func["train"] = _TrainFunction(self.engine)
         for key in self.data.generate_split_keys():
             ds = self.engine.split if key == "train" else DeviceSplit(self.data.split[key], self.device)

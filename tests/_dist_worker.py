@@ -44,6 +44,27 @@ def _dataset():
     return synthetic_dataset(DP_SHAPE["N"], DP_SHAPE["d"], DP_SHAPE["ntrue"], seed=DP_SHAPE["seed"])
 
 
+# the DP_SHAPE set relabelled into vocabularies whose owned rows per rank exceed the row
+# lists' LDS bitmap (32 * RAE_DPL_KEYS = 524288 rows at G = 2): entity e -> e * BIG_E, feature
+# f -> f * BIG_F, so k_build_dplists takes its hash-pass path for both tables
+BIG_E, BIG_F = 25013, 5243
+
+
+def _dataset_big():
+    import scipy.sparse as sp
+    from rae.data import DatasetManager, DatasetSplit
+    data, gold = _dataset()
+    n, d = data.get_arg_voc_size(), data.get_dimensionality()
+    splits = {}
+    for k, v in data.split.items():
+        x = v.xFeats.tocoo()
+        xb = sp.csr_matrix((x.data, (x.row, x.col * BIG_F)), shape=(x.shape[0], d * BIG_F))
+        splits[k] = DatasetSplit(v.args1 * BIG_E, v.args2 * BIG_E, xb)
+    freqs = np.zeros(n * BIG_E, dtype=np.int64)
+    freqs[np.arange(n) * BIG_E] = data.entity_freqs
+    return DatasetManager(splits, freqs, d * BIG_F), gold
+
+
 def run_exchange(out):
     from rae import dist as rdist
     ws, rk = dist.get_world_size(), dist.get_rank()
@@ -186,13 +207,13 @@ def run_sync_rows(out):
 
 
 def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", index_window=0,
-            xchg="collective", graph_chunk=1):
+            xchg="collective", graph_chunk=1, vocab="small"):
     from rae import dist as rdist
     from rae.inducer import ReconstructInducer
     ws, rk = dist.get_world_size(), dist.get_rank()
     dev = torch.device("cuda", 0)                 # both ranks share the one GPU of the box
     torch.cuda.set_device(dev)
-    data, gold = _dataset()
+    data, gold = _dataset_big() if vocab == "big" else _dataset()
     m, r, s, l = DP_SHAPE["m"], DP_SHAPE["r"], DP_SHAPE["s"], DP_SHAPE["l"]
     ex = rdist.make_exchange(ws, rk)
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), DP_SHAPE["epochs"], 0.1, l, r,
@@ -212,6 +233,8 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", ind
     ind.engine.sync_replicas()
     params = {k: v.detach().cpu().double().numpy() for k, v in ind.modelFunc.named_params().items()}
     tag = dp_update if xchg == "collective" else f"{dp_update}_{xchg}"
+    if vocab != "small":
+        tag += "_" + vocab
     np.savez(os.path.join(out, f"gpu_{tag}_{decoder}_{rk}.npz"),
              costs=np.concatenate(ind.epoch_costs), **params)
 
@@ -417,7 +440,8 @@ def main():
                     sys.argv[6] if len(sys.argv) > 6 else "auto",
                     int(sys.argv[7]) if len(sys.argv) > 7 else 0,
                     sys.argv[8] if len(sys.argv) > 8 else "collective",
-                    int(sys.argv[9]) if len(sys.argv) > 9 else 1)
+                    int(sys.argv[9]) if len(sys.argv) > 9 else 1,
+                    sys.argv[10] if len(sys.argv) > 10 else "small")
         elif mode == "gpu_c3":
             run_gpu_c3(out, dp_update=dec if dec != "sp" else "replicated",
                        heavy_chunk=sys.argv[4] if len(sys.argv) > 4 else "auto")

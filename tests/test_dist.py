@@ -160,6 +160,29 @@ def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dens
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("xchg", ["collective", "p2p"])
+def test_gpu_partitioned_large_vocabulary(built_lib, cuda_dev, tmp_path, xchg):
+    """vocabularies whose owned rows exceed the row lists' LDS bitmap take
+    k_build_dplists' hash passes (sized from the owned candidates, restarted with more passes
+    when one overflows); the partitioned update on two ranks (both exchanges) is bitwise equal
+    to the replicated one on the same relabelled data -- a missing or stale row in a list would
+    change the trajectory."""
+    from _dist_worker import BIG_E, BIG_F
+    data, _ = _dataset()
+    n, d = data.get_arg_voc_size() * BIG_E, data.get_dimensionality() * BIG_F
+    assert min(n, d) // 2 > 32 * 16384          # rae_dp.hpp: nq > 32 * RAE_DPL_KEYS, G = 2
+    _launch(["gpu", str(tmp_path), "sp", "partitioned", "auto", "auto", "0", xchg, "1", "big"])
+    _launch(["gpu", str(tmp_path), "sp", "replicated", "auto", "auto", "0", "collective", "1",
+             "big"])
+    tag = "partitioned" if xchg == "collective" else "partitioned_p2p"
+    gp = [np.load(tmp_path / f"gpu_{tag}_big_sp_{k}.npz") for k in range(2)]
+    gr = np.load(tmp_path / "gpu_replicated_big_sp_0.npz")
+    for k in gr.files:
+        np.testing.assert_array_equal(gp[0][k], gp[1][k], err_msg=k)
+        np.testing.assert_array_equal(gp[0][k], gr[k], err_msg=k)
+
+
+@pytest.mark.gpu
 def test_partitioned_gather_then_rank0_checkpoint(built_lib, cuda_dev, tmp_path):
     """under the partitioned update a checkpoint from rank 0 alone must not start a
     collective.  Every rank calls ReconstructInducer.gather(); rank 0 then saves and labels by
@@ -231,10 +254,11 @@ def _c4dp_reference(cuda_dev, ws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 4, 8])
 def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
-    """BASELINE config 4's data-parallel kernel combination -- K = 300,
-    embed 300, neg 50, l = 100 per rank: the split SP forward, the wire records (dw1 / dw2 per
+    """BASELINE config 4's data-parallel kernel combination --
+    K = 300, embed 300, neg 50, l = 100 per rank, up to the 8 ranks of the config (global batch
+    800, L = 800 update with 102 record slots): the split SP forward, the wire records (dw1 / dw2 per
     example), k_vrec and 102 record slots with private rows off -- on `ws` ranks sharing the GPU
     (gloo), both update forms, the partitioned one also over the peer-to-peer exchange (the
     worker asserts the resolved forms).  Checked:

@@ -113,3 +113,25 @@ def test_bench_attaches_traffic_of_the_same_batch_size():
     t8 = bench.pmc_traffic("c3", 800)
     assert t8 is not None and "--batch-size 800" in t8["source"]
     assert bench.pmc_traffic("c3", 37) is None
+
+
+def test_p2p_device_guard():
+    """the peer-to-peer exchange refuses ranks on different GPUs unless asked
+    (engine.check_p2p_devices, called by TrainEngine._p2p_setup with every rank's device)."""
+    from rae.engine import check_p2p_devices
+    check_p2p_devices(["gpu-a"] * 8, False)              # ranks sharing one GPU
+    with pytest.raises(ValueError, match="p2p_cross_device"):
+        check_p2p_devices(["gpu-a", "gpu-b"], False)
+    check_p2p_devices(["gpu-a", "gpu-b"], True)
+
+
+def test_integration_names_every_export():
+    """every entry point include/rae.h declares has its binding row or
+    recipe in INTEGRATION.md."""
+    import re
+    from conftest import ROOT
+    from test_abi import header_symbols
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    named = set(re.findall(r"\b(rae_[a-z_0-9]+)", doc))
+    missing = [s for s in header_symbols() if s not in named]
+    assert not missing, missing

@@ -111,3 +111,25 @@ def test_build_is_warning_free(built_lib):
         pytest.skip("library built without a log (prebuilt)")
     log = open(BUILD_LOG).read()
     assert "warning:" not in log, log[:2000]
+
+
+P2P_PUSHES = ("_Z10k_p2p_rowsN3rae8StepArgsE", "_Z10k_p2p_recsN3rae8StepArgsE")
+
+
+def test_p2p_pushes_store_write_through_at_system_scope(disasm):
+    """rae_p2p.hpp "Visibility across GPUs", producer side: every store of the push kernels
+    into a peer's memory is a system-scope write-through (sc0 sc1), and the waves end only
+    through a vmcnt(0) wait -- no pushed byte is left dirty in one of this GPU's L2s, or in
+    flight, when the signal kernel that follows runs."""
+    for name in P2P_PUSHES:
+        code = disasm.get(name)
+        assert code, f"{name} is not in the code object"
+        stores = [c for c in code if c.startswith("global_store")]
+        assert stores, name
+        for c in stores:
+            assert re.search(r"\bsc0\b", c) and re.search(r"\bsc1\b", c), c
+        ends = [i for i, c in enumerate(code) if c.startswith("s_endpgm")]
+        assert ends, name
+        for i in ends:
+            assert code[i - 1].startswith("s_waitcnt") and "vmcnt(0)" in code[i - 1], \
+                (name, code[i - 1])

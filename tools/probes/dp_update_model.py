@@ -53,6 +53,9 @@ class NoPeers:
     def sync_rows(self, ts):
         pass
 
+    def barrier(self):
+        pass
+
 
 def loopback_p2p_setup(eng):
     """Peers of a G-rank plan with no peer processes: every peer's exchange buffer / replica
