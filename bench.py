@@ -261,7 +261,7 @@ def main():
     ap.add_argument("--dp-update", default="replicated", choices=["replicated", "partitioned"],
                     help="data-parallel update (N > 1): every rank updates every row, or each "
                          "rank the rows it owns (rows pulled from their owners each step)")
-    ap.add_argument("--dp-xchg", default="collective", choices=["collective", "p2p"],
+    ap.add_argument("--dp-xchg", default="collective", choices=["collective", "p2p", "p2p_pipe"],
                     help="partitioned update, N > 1: RCCL collectives between the step launches, or "
                          "the kernels' own stores into the peers' IPC-mapped buffers (include/rae.h "
                          "RAE_XCHG_P2P)")
@@ -269,9 +269,9 @@ def main():
                     help="--dp-xchg p2p with ranks on different GPUs (verified on ranks sharing "
                          "one GPU only; refused without this flag)")
     args = ap.parse_args()
-    if args.dp_xchg == "p2p":
+    if args.dp_xchg != "collective":
         args.dp_update = "partitioned"
-        args.kernel_form.append("dp_xchg=p2p")
+        args.kernel_form.append(f"dp_xchg={args.dp_xchg}")
 
     import torch
     from rae import dist as rdist
@@ -321,9 +321,11 @@ def main():
     # ahead.  Here it is built for the warm-up + timed batches before the timed region, and
     # its per-batch cost over a whole window (how the epoch loop pays it) is added to the
     # timed seconds for the headline value.
-    prebuilt = W + K <= eng.index_window
+    # (the pipelined peer-to-peer form's last step reads the row lists of the batch after it)
+    look = min(eng._look, nb - W - K)
+    prebuilt = W + K + look <= eng.index_window
     if prebuilt:
-        eng.build_index(0, W + K)
+        eng.build_index(0, W + K + look)
         eng.check()                        # a partition overflow is reported before any step
     if eng._dp:                            # the rows all-to-all's communicator, before capture
         if not prebuilt:

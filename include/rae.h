@@ -141,6 +141,11 @@ typedef struct rae_config {
 #define RAE_XCHG_P2P 1        /* partitioned update only: the kernels store records and rows     *
                                * straight into the peers' buffers (rae_set_peer) and wait on     *
                                * their signal counters -- no caller collective in the step       */
+#define RAE_XCHG_P2P_PIPE 2   /* RAE_XCHG_P2P with the next batch's rows pushed during this step: *
+                               * the rows the update leaves unchanged right after the forward,   *
+                               * every updated row by the update task that writes it -- so the   *
+                               * row bytes travel under the update; world_size <= 8, private     *
+                               * rows off; rae_p2p_prologue before the first step of a run       */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]
@@ -273,6 +278,12 @@ int rae_set_peer(rae_plan* plan, int32_t peer, float* exchange_dev, float* W_dev
  * gives up (default 5 s; a driver that does host work between steps -- per-batch evaluation
  * -- raises it or puts a host barrier in front of the next step)                          */
 int rae_set_p2p_timeout(rae_plan* plan, double seconds);
+/* RAE_XCHG_P2P_PIPE: each step pushes (and signals) the rows of the NEXT batch, so the first
+ * step of a run needs its own batch's rows pushed first: marks and pushes the rows of
+ * `batch` and signals them (every rank calls it with the same batch).  drain != 0: the step
+ * before this run pushed rows for another batch -- consume that signal first.  The row index
+ * (rae_build_index) of a step's batch + 1 must be built before the step runs.            */
+int rae_p2p_prologue(rae_plan* plan, int64_t batch, int32_t drain, rae_stream_t stream);
 
 /* Kernel timing (bench / profiling; no reference counterpart).  Arms the NEXT
  * rae_step_forward or rae_step_update call on this plan: its kernels are launched with

@@ -201,6 +201,9 @@ __global__ __launch_bounds__(RAE_FBT) void k_build_dplists(StepArgs a, int64_t f
 // peer-to-peer exchange (rae_p2p.hpp)
 __global__ __launch_bounds__(RAE_BT) void k_p2p_recs(StepArgs a) { p2p_push_records(a); }
 __global__ __launch_bounds__(RAE_BT) void k_p2p_rows(StepArgs a) { p2p_push_rows(a); }
+__global__ __launch_bounds__(RAE_BT) void k_p2p_pre(StepArgs a, int prologue, int nmb) {
+    p2p_pre(a, prologue, nmb);
+}
 __global__ __launch_bounds__(64) void k_p2p_signal(StepArgs a, int kind) { p2p_signal(a, kind); }
 __global__ __launch_bounds__(64) void k_p2p_wait(StepArgs a, int kind, unsigned per) {
     p2p_wait(a, kind, per);
@@ -702,14 +705,19 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_ON ||
         c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS ||
         c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON ||
-        c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P)
+        c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P_PIPE)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
                                    "priv_rows / dp_dense / heavy_chunk / dp_xchg)");
-    if (c.dp_xchg == RAE_XCHG_P2P && (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31 ||
-                                      c.embed % 4 || c.relations % 4 || c.embed > 512 ||
-                                      c.relations > 512))
+    if (c.dp_xchg != RAE_XCHG_COLLECTIVE &&
+        (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31 || c.embed % 4 ||
+         c.relations % 4 || c.embed > 512 || c.relations > 512))
         return fail(RAE_E_INVALID, "the peer-to-peer exchange runs the partitioned update "
                                    "(world_size <= 31; embed and relations multiples of 4, <= 512)");
+    // the pipelined form marks a row's reading peers in one byte, and its update pushes rows
+    // from the row tasks only (not from the private-row tasks)
+    if (c.dp_xchg == RAE_XCHG_P2P_PIPE && (c.world_size > 8 || c.priv_rows == RAE_PRIV_ON))
+        return fail(RAE_E_INVALID, "the pipelined peer-to-peer exchange needs world_size <= 8 and "
+                                   "private rows off");
     if (c.bil_dp == RAE_BILDP_MTILE && !(c.decoder != RAE_DEC_SP && c.mfma_bf16 && c.relations <= 128))
         return fail(RAE_E_INVALID, "bil_dp MTILE needs a bf16 bilinear plan with relations <= 128");
     if (c.dp_update == RAE_DPUPD_PARTITIONED && (c.lambda1 != 0.f || c.lambda2 != 0.f))
@@ -920,6 +928,11 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     // peer-to-peer exchange: the peers' mapped buffers and this rank's expected signal counts
     const size_t o_peers = take(sizeof(PeerBufs) * (size_t)c.world_size);
     const size_t o_pexp = take(4ull * 2 * c.world_size);
+    // pipelined peer-to-peer form: two parities of row-mark bytes over the owned rows
+    a.pipe = (c.dp_xchg == RAE_XCHG_P2P_PIPE && c.world_size > 1) ? 1 : 0;
+    a.pmA = a.pipe ? (int)((((c.n_entities + c.world_size - 1) / c.world_size + 3) / 4 + 3) & ~3) : 0;
+    a.pmW = a.pipe ? (int)((((c.n_features + c.world_size - 1) / c.world_size + 3) / 4 + 3) & ~3) : 0;
+    const size_t o_pm = a.pipe ? take(4ull * 2 * (a.pmA + a.pmW)) : 0;
     const bool bil = c.decoder != RAE_DEC_SP;
     a.bf16 = (bil && c.mfma_bf16) ? 1 : 0;
     // bf16 dP with LDS-staged R slices (k_bil_dp2): the C5 shape compiled exactly, other
@@ -971,7 +984,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         return fail(RAE_E_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     }
     *p->h_err = 0;
-    if (c.dp_xchg == RAE_XCHG_P2P) {
+    if (c.dp_xchg != RAE_XCHG_COLLECTIVE) {
         // the peers add to these words over xGMI and this rank polls them: uncached (no L2
         // line of them can go stale; rae_p2p.hpp "Visibility across GPUs")
         e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p->d_sig), 4ull * 2 * c.world_size,
@@ -1021,6 +1034,7 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     a.xchg = c.dp_xchg;
     a.peers = reinterpret_cast<PeerBufs*>(p->ws + o_peers);
     a.p2p_expect = reinterpret_cast<unsigned*>(p->ws + o_pexp);
+    a.pm = a.pipe ? reinterpret_cast<uint32_t*>(p->ws + o_pm) : nullptr;
     a.pmask = a.priv ? reinterpret_cast<int32_t*>(p->ws + o_pmask) : nullptr;
     if (a.lay.wire) a.vb = reinterpret_cast<float*>(p->ws + o_vb);
     if (a.dpart) a.dwb = reinterpret_cast<float*>(p->ws + o_dwb);
@@ -1237,7 +1251,13 @@ static unsigned p2p_recs_grid(const StepArgs& a) {
     const int64_t g = ((int64_t)a.l * a.lay.rec / 4 + RAE_BT - 1) / RAE_BT;
     return (unsigned)(g < 1 ? 1 : g);
 }
-static bool p2p_on(const rae_plan* p) { return p->args.xchg == RAE_XCHG_P2P && p->args.G > 1; }
+static bool p2p_on(const rae_plan* p) { return p->args.xchg != RAE_XCHG_COLLECTIVE && p->args.G > 1; }
+// k_p2p_pre's grid: marking threads (one per list entry of every list, the own one included)
+// + pushing waves (one per entry of the peers' lists)
+static int p2p_pre_mark_blocks(const StepArgs& a) {
+    const int64_t n = (int64_t)a.G * (a.capA + a.capW);
+    return (int)((n + RAE_BT - 1) / RAE_BT);
+}
 
 static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
     if (!p->args.neg1 || !p->args.neg2) return fail(RAE_E_STATE, "negatives not set");
@@ -1246,11 +1266,13 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     a.step_offset = off;
     a.stamps = p->stamps_fwd;
     const bool p2p = p2p_on(p);
-    if (p2p) {                // the owned rows the peers' examples read, into their replicas
+    if (p2p) {
         if (!p->peers_set) return fail(RAE_E_STATE, "peer buffers not set (rae_set_peer)");
-        const unsigned gr = p2p_rows_grid(a);     // (>= 1 workgroup: the signal follows anyway)
-        RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_BT), 0, st, a);
-        RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 1);
+        if (!a.pipe) {        // the owned rows the peers' examples read, into their replicas
+            const unsigned gr = p2p_rows_grid(a);   // (>= 1 workgroup: the signal follows anyway)
+            RAE_LAUNCH(p, k_p2p_rows, dim3(gr), dim3(RAE_BT), 0, st, a);
+            RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 1);
+        }                     // pipelined: pushed and signalled by the previous step / prologue
         RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, 1u);
     }
     if (a.dec == RAE_DEC_SP) {
@@ -1262,8 +1284,13 @@ static int launch_forward(rae_plan* p, const int64_t* cursor, int64_t off, hipSt
     else launch_fwd_bil<false>(p, a, st);
     if (p2p)                  // this rank's records into every peer's exchange buffer
     {
-        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a)), dim3(RAE_BT), 0, st, a);
+        // (pipelined: + blocks clearing the next batch's row marks)
+        RAE_LAUNCH(p, k_p2p_recs, dim3(p2p_recs_grid(a) + (a.pipe ? 64 : 0)), dim3(RAE_BT), 0, st, a);
         RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 0);
+        if (a.pipe) {         // the next batch's rows this step's update leaves unchanged
+            const int nmb = p2p_pre_mark_blocks(a);
+            RAE_LAUNCH(p, k_p2p_pre, dim3(nmb + p2p_rows_grid(a)), dim3(RAE_BT), 0, st, a, 0, nmb);
+        }
     }
     p->t_start = p->t_stop = nullptr;
     HIPCHK(hipGetLastError());
@@ -1366,6 +1393,10 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
         RAE_LAUNCH(p, k_finalize_cost, dim3(1), dim3(64), 0, st, a);
         HIPCHK(hipGetLastError());
     }
+    if (p2p_on(p) && a.pipe) {   // the next batch's rows are in the peers' replicas
+        RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 1);
+        HIPCHK(hipGetLastError());
+    }
     p->t_start = p->t_stop = nullptr;
     return RAE_OK;
 }
@@ -1452,7 +1483,7 @@ extern "C" int rae_set_dp_buffers(rae_plan* p, float* send, float* recv, int32_t
                                   int32_t cap_features) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
     if (!p->args.part) return fail(RAE_E_STATE, "the plan's data-parallel update is not partitioned");
-    if ((p->args.xchg != RAE_XCHG_P2P && (!send || !recv)) || cap_entities < 0 || cap_features < 0 ||
+    if ((p->args.xchg == RAE_XCHG_COLLECTIVE && (!send || !recv)) || cap_entities < 0 || cap_features < 0 ||
         cap_entities > p->args.LA || cap_features > p->args.LW)
         return fail(RAE_E_INVALID, "bad row-exchange buffers / capacities");
     StepArgs& a = p->args;
@@ -1539,7 +1570,7 @@ extern "C" void* rae_p2p_signals(rae_plan* p) { return p ? (void*)p->d_sig : nul
 extern "C" int rae_set_peer(rae_plan* p, int32_t peer, float* exchange, float* W, float* A,
                             float* Ab, void* signals) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
-    if (p->args.xchg != RAE_XCHG_P2P) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
+    if (p->args.xchg == RAE_XCHG_COLLECTIVE) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
     if (peer < 0 || peer >= p->args.G || peer == p->args.rank)
         return fail(RAE_E_INVALID, "peer must be another rank");
     if (!exchange || !W || !A || !Ab || !signals) return fail(RAE_E_INVALID, "null peer buffer");
@@ -1549,9 +1580,28 @@ extern "C" int rae_set_peer(rae_plan* p, int32_t peer, float* exchange, float* W
     p->peers_set = p->peers_mask == (((1 << p->args.G) - 1) & ~(1 << p->args.rank));
     return RAE_OK;
 }
+extern "C" int rae_p2p_prologue(rae_plan* p, int64_t batch, int32_t drain, rae_stream_t stream) {
+    if (!p) return fail(RAE_E_INVALID, "null plan");
+    if (!p2p_on(p) || !p->args.pipe)
+        return fail(RAE_E_STATE, "the plan's exchange is not the pipelined peer-to-peer form");
+    if (!p->peers_set) return fail(RAE_E_STATE, "peer buffers not set (rae_set_peer)");
+    if (int rc = check_batch(p, batch)) return rc;
+    const hipStream_t st = (hipStream_t)stream;
+    StepArgs a = p->args;
+    a.cursor = nullptr;
+    a.step_offset = batch;
+    if (drain)                // the signal of rows a previous step pushed for another batch
+        RAE_LAUNCH(p, k_p2p_wait, dim3(1), dim3(64), 0, st, a, 1, 1u);
+    HIPCHK(hipMemsetAsync(a.pm, 0, 4ull * 2 * (a.pmA + a.pmW), st));
+    const int nmb = p2p_pre_mark_blocks(a);
+    RAE_LAUNCH(p, k_p2p_pre, dim3(nmb + p2p_rows_grid(a)), dim3(RAE_BT), 0, st, a, 1, nmb);
+    RAE_LAUNCH(p, k_p2p_signal, dim3(1), dim3(64), 0, st, a, 1);
+    HIPCHK(hipGetLastError());
+    return RAE_OK;
+}
 extern "C" int rae_set_p2p_timeout(rae_plan* p, double seconds) {
     if (!p) return fail(RAE_E_INVALID, "null plan");
-    if (p->args.xchg != RAE_XCHG_P2P) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
+    if (p->args.xchg == RAE_XCHG_COLLECTIVE) return fail(RAE_E_STATE, "the plan's exchange is not peer-to-peer");
     if (!(seconds > 0.0) || seconds > 3600.0) return fail(RAE_E_INVALID, "timeout must be in (0, 3600] s");
     p->args.p2p_timeout = (unsigned long long)(seconds * 1e8);   // s_memrealtime: 100 MHz
     return RAE_OK;

@@ -544,6 +544,34 @@ __device__ __forceinline__ float mt_sum(const float* part, int q0, int q1, int l
     for (; q < q1; ++q) t0 += p[q * st];
     return (t0 + t1) + (t2 + t3);
 }
+// the same sum with every partial's load issued at once (q1 - q0 <= NMAX; q0 is a valid block
+// index): one memory round trip instead of one per four partials, and exactly mt_sum's adds
+// in mt_sum's order -- chains t0..t3 over the full groups of four, the rest into t0
+template <int NMAX>
+__device__ __forceinline__ float mt_sum_1rt(const float* part, int q0, int q1, int l, int r4, int b, int i) {
+    const int n = q1 - q0;
+    if (n > NMAX) return mt_sum(part, q0, q1, l, r4, b, i);
+    const float* p = part + (int64_t)b * r4 + i;
+    const int64_t st = (int64_t)l * r4;
+    float v[NMAX];
+#pragma unroll
+    for (int u = 0; u < NMAX; ++u) v[u] = p[(int64_t)(q0 + (u < n ? u : 0)) * st];
+    const int nf = n & ~3;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+    for (int u = 0; u < NMAX; u += 4) {
+        if (u < nf) {
+            t0 += v[u];
+            t1 += v[u + 1];
+            t2 += v[u + 2];
+            t3 += v[u + 3];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NMAX; ++u)
+        if (u >= nf && u < n) t0 += v[u];
+    return (t0 + t1) + (t2 + t3);
+}
 // One example's M-tile sums with four threads per element i: quarter qd of the workgroup's
 // index space sums half the partials of one output -- qd 0/1: the j-block partials (mtV),
 // qd 2/3: the i-block partials (mtW) -- into q0v / q1v / q0w / q1w; the caller combines the
@@ -556,8 +584,8 @@ __device__ __forceinline__ void mt_sums_split(const StepArgs& a, int b, float* q
     for (int e = threadIdx.x; e < 4 * r4; e += T) {
         const int qd = e / r4, i = e - qd * r4;
         const int n = qd < 2 ? nbj : nbi, h = n / 2;
-        const float t = i < r ? mt_sum(qd < 2 ? a.mtV : a.mtW, (qd & 1) ? h : 0, (qd & 1) ? n : h,
-                                       a.l, r4, b, i) : 0.f;
+        const float t = i < r ? mt_sum_1rt<16>(qd < 2 ? a.mtV : a.mtW, (qd & 1) ? h : 0,
+                                               (qd & 1) ? n : h, a.l, r4, b, i) : 0.f;
         (qd == 0 ? q0v : qd == 1 ? q1v : qd == 2 ? q0w : q1w)[i] = t;
     }
 }
@@ -1030,6 +1058,7 @@ __device__ void bil_gemm_dp(const StepArgs& a, int t, int lane) {
 // thread has ~nib / NS independent loads instead of nib.
 #define RAE_FINT 1024
 #define RAE_FINW (RAE_FINT / RAE_WAVE)
+#define RAE_FIN_Q 40     // dP partials per split summed from one round of loads
 __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, float* red) {
     const int m = a.m, r = a.r, l = a.l;
     const bool hybrid = a.dec == 2;
@@ -1045,14 +1074,26 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, fl
         const int sp = e / m, k = e - sp * m;
         const float* pp = pbase + (int64_t)bl * m + k;
         const int64_t st = (int64_t)l * m;
-        // eight independent chains (fixed order): the loads of eight partials issue together
+        // eight independent chains, fixed order: chain u sums partials sp + NS q, q = u mod 8,
+        // in increasing q.  Up to RAE_FIN_Q partials per split: every load issued at once (one
+        // round trip, clamped addresses), then the adds in that order
         float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int ib = sp;
-        for (; ib + 7 * NS < npart; ib += 8 * NS) {
+        const int nper = sp < npart ? (npart - sp + NS - 1) / NS : 0;
+        if (nper <= RAE_FIN_Q) {
+            float v[RAE_FIN_Q];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] += pp[(ib + u * NS) * st];
+            for (int q = 0; q < RAE_FIN_Q; ++q) v[q] = pp[(int64_t)(q < nper ? sp + q * NS : 0) * st];
+#pragma unroll
+            for (int q = 0; q < RAE_FIN_Q; ++q)
+                if (q < nper) t[q & 7] += v[q];
+        } else {
+            int ib = sp;
+            for (; ib + 7 * NS < npart; ib += 8 * NS) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t[u] += pp[(ib + u * NS) * st];
+            }
+            for (int u = 0; ib < npart; ib += NS, ++u) t[u] += pp[ib * st];
         }
-        for (int u = 0; ib < npart; ib += NS, ++u) t[u] += pp[ib * st];
         sdp[e] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
     mt_sums_split<RAE_FINT>(a, bl, smt, smt + 1024, smt + 2048, smt + 3072);

@@ -56,7 +56,9 @@ __device__ void build_dp_list(const StepArgs& a, int64_t g, int64_t slot, int di
     const int G = a.G;
     const int x = dir == 0 ? p : a.rank, y = dir == 0 ? a.rank : p;
     int32_t* cnt_out = dpl_count(a, slot, dir, p, tab);
-    if (p == a.rank) {                                          // own rows: nothing travels
+    // own rows: nothing travels -- but the pipelined peer-to-peer form marks the rows its own
+    // examples read too (rae_p2p.hpp: a batch's marks are the rows its update writes)
+    if (p == a.rank && !(a.pipe && dir == 0)) {
         if (tid == 0) *cnt_out = 0;
         return;
     }

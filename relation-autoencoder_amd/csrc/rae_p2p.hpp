@@ -75,9 +75,22 @@ __device__ void p2p_signal(const StepArgs& a, int kind) {
     }
 }
 
-// k_p2p_recs: this rank's l records (float4 slices) into every peer's buffer
+// k_p2p_recs: this rank's l records (float4 slices) into every peer's buffer.  Pipelined form:
+// the blocks past the records clear the row marks of batch b + 1's parity (they held batch
+// b - 1's, whose last readers -- the pre-push of step b - 1, the update of b - 2 -- are done),
+// which k_p2p_pre of this step then fills
 __device__ void p2p_push_records(const StepArgs& a) {
     const int64_t n4 = (int64_t)a.l * a.lay.rec / 4;                 // rec is a multiple of 4
+    const int64_t nrb = (n4 + blockDim.x - 1) / blockDim.x;
+    if (a.pipe && (int64_t)blockIdx.x >= nrb) {
+        const int64_t b = step_batch(a);
+        uint4* pm = reinterpret_cast<uint4*>(a.pm + (int64_t)((b + 1) & 1) * (a.pmA + a.pmW));
+        const int64_t nw4 = (a.pmA + a.pmW) / 4;                      // pmA, pmW multiples of 4
+        for (int64_t i = (blockIdx.x - nrb) * blockDim.x + threadIdx.x; i < nw4;
+             i += (gridDim.x - nrb) * blockDim.x)
+            pm[i] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
     const int64_t o4 = (int64_t)a.rank * a.l * a.lay.rec / 4;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
@@ -85,6 +98,21 @@ __device__ void p2p_push_records(const StepArgs& a) {
     for (int p = 0; p < a.G; ++p)
         if (p != a.rank) store_sys(reinterpret_cast<float4*>(a.peers[p].ex) + o4 + i, v);
     p2p_stores_done();
+}
+
+// one owned row of table tab into peer p's replica (one wave; Ab with the entity rows)
+__device__ __forceinline__ void push_row_to(const StepArgs& a, int p, int tab, int row, int lane) {
+    const int w = tab ? a.m : a.r;                   // r, m multiples of 4, <= 512
+    const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
+    float4* d = reinterpret_cast<float4*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
+    const int w4 = w / 4;
+    float4 v0, v1;
+    if (lane < w4) v0 = s[lane];
+    if (lane + 64 < w4) v1 = s[lane + 64];
+    const float ab = (!tab && lane == 0) ? a.Ab[row] : 0.f;
+    if (lane < w4) store_sys(d + lane, v0);
+    if (lane + 64 < w4) store_sys(d + lane + 64, v1);
+    if (!tab && lane == 0) store_sys(a.peers[p].Ab + row, ab);
 }
 
 // k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
@@ -105,18 +133,101 @@ __device__ void p2p_push_rows(const StepArgs& a) {
     const int row = dpl_list(a, slot, 0, p, tab)[i < cap ? i : 0];
     if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
     if (i >= n || i >= cap) return;
-    const int w = tab ? a.m : a.r;                   // r, m multiples of 4, <= 512
-    const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
-    float4* d = reinterpret_cast<float4*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
-    const int w4 = w / 4;
-    float4 v0, v1;
-    if (lane < w4) v0 = s[lane];
-    if (lane + 64 < w4) v1 = s[lane + 64];
-    const float ab = (!tab && lane == 0) ? a.Ab[row] : 0.f;
-    if (lane < w4) store_sys(d + lane, v0);
-    if (lane + 64 < w4) store_sys(d + lane + 64, v1);
-    if (!tab && lane == 0) store_sys(a.peers[p].Ab + row, ab);
+    push_row_to(a, p, tab, row, lane);
     p2p_stores_done();
+}
+
+// ---- pipelined form (RAE_XCHG_P2P_PIPE) ------------------------------------------------------
+// The rows peer p's examples read in batch b + 1 (direction-0 list) leave during step b:
+//   k_p2p_pre(b), right after the forward and the record push: marks batch b + 1's lists into
+//     the row-mark bytes of its parity (bit p per list p, the own list included), and pushes the
+//     listed rows that batch b does NOT update (mark byte of b's parity == 0: no list of b holds
+//     the row, so no row task of update(b) writes it) -- final values, pushed while the peers'
+//     records are still on their way;
+//   update(b): every row task, as it writes an owned row, stores it into each peer whose bit is
+//     set in batch b + 1's mark byte (pipe_push_row) -- the updated rows travel under the update;
+//   k_p2p_signal (kind 1) after the update: batch b + 1's rows are all in place.
+// A run's first batch has no previous step: rae_p2p_prologue marks and pushes its whole lists.
+// Hazards: a pre-pushed row is one update(b) leaves alone, so its value equals what a peer
+// that reads it in batch b already holds (an identical overwrite while that peer's forward(b)
+// may read it); an update push reaches a peer after its forward(b) (this rank's update waited
+// for the peer's records of b) and before its forward(b + 1) (which waits for kind 1).
+__device__ __forceinline__ uint8_t* pipe_marks(const StepArgs& a, int64_t batch, int tab) {
+    return reinterpret_cast<uint8_t*>(a.pm + (batch & 1) * (int64_t)(a.pmA + a.pmW) + (tab ? a.pmA : 0));
+}
+__device__ __forceinline__ int64_t epoch_batches(const StepArgs& a) { return a.N / a.L; }
+
+// k_p2p_pre: blocks [0, nmb): one thread per list entry marks batch tb's lists; the rest: one
+// wave per (peer, list entry) pushes -- prologue: every listed row of tb = step_batch; else tb =
+// step_batch + 1 and only the rows step_batch does not update
+__device__ void p2p_pre(const StepArgs& a, int prologue, int nmb) {
+    const int64_t b = step_batch(a);
+    const int64_t tb = prologue ? b : b + 1;
+    if (tb >= epoch_batches(a)) return;               // the epoch's last step: nothing follows
+    const int64_t slot = tb % a.index_window;
+    const int per = a.capA + a.capW;
+    if ((int)blockIdx.x < nmb) {
+        const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
+        if (p >= a.G) return;
+        const int tab = i0 >= a.capA ? 1 : 0;
+        const int i = tab ? i0 - a.capA : i0;
+        const int cap = tab ? a.capW : a.capA;
+        const int n = *dpl_count(a, slot, 0, p, tab);
+        if (i == 0 && n > cap) atomicOr(a.err, 16);
+        if (i >= n || i >= cap) return;
+        const int q = dpl_list(a, slot, 0, p, tab)[i] / a.G;
+        uint32_t* w = reinterpret_cast<uint32_t*>(pipe_marks(a, tb, tab)) + (q >> 2);
+        atomicOr(w, (1u << p) << (8 * (q & 3)));
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)(blockIdx.x - nmb) * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int p = (int)(t / per), i0 = (int)(t - (int64_t)p * per);
+    if (p >= a.G || p == a.rank) return;
+    const int tab = i0 >= a.capA ? 1 : 0;
+    const int i = tab ? i0 - a.capA : i0;
+    const int cap = tab ? a.capW : a.capA;
+    const int n = *dpl_count(a, slot, 0, p, tab);
+    const int row = dpl_list(a, slot, 0, p, tab)[i < cap ? i : 0];
+    if (i == 0 && lane == 0 && n > cap) atomicOr(a.err, 16);
+    if (i >= n || i >= cap) return;
+    if (!prologue && pipe_marks(a, b, tab)[row / a.G] != 0) return;   // update(b) pushes it
+    push_row_to(a, p, tab, row, lane);
+    p2p_stores_done();
+}
+
+// update(b), pipelined form: owned row `row` of table tab was just written (its new values in
+// the lanes' vectors v[0..Q)): into the replica of every peer that reads it in batch b + 1
+template <class VT, int Q>
+__device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int row, const VT (&v)[Q],
+                                              int nv, int lane) {
+    if (!a.pipe) return;
+    const int64_t tb = step_batch(a) + 1;
+    if (tb >= epoch_batches(a)) return;
+    const unsigned mk = pipe_marks(a, tb, tab)[row / a.G] & ~(1u << a.rank);
+    if (!mk) return;
+    constexpr int VW = sizeof(VT) / sizeof(float);
+    const int w = tab ? a.m : a.r;
+    for (int p = 0; p < a.G; ++p) {
+        if (!((mk >> p) & 1u)) continue;
+        VT* d = reinterpret_cast<VT*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int c = lane + RAE_WAVE * q;
+            if (c < nv) store_sys(d + c, v[q]);
+        }
+    }
+    (void)VW;
+}
+// ... and an entity row's Ab (lane 0)
+__device__ __forceinline__ void pipe_push_ab(const StepArgs& a, int row, float v) {
+    if (!a.pipe) return;
+    const int64_t tb = step_batch(a) + 1;
+    if (tb >= epoch_batches(a)) return;
+    const unsigned mk = pipe_marks(a, tb, 0)[row / a.G] & ~(1u << a.rank);
+    for (int p = 0; p < a.G; ++p)
+        if ((mk >> p) & 1u) store_sys(a.peers[p].Ab + row, v);
 }
 
 // k_p2p_wait: lane p waits for peer p's `per` signals of this step (kind 0 records, 1 rows):

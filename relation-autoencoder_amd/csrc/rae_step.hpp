@@ -217,6 +217,12 @@ struct StepArgs {
     unsigned* sig;       // uncached allocation (rae.hip: hipDeviceMallocUncached)
     unsigned* p2p_expect;
     unsigned long long p2p_timeout;   // s_memrealtime ticks (100 MHz) a wait may spin
+    // pipelined form (RAE_XCHG_P2P_PIPE, rae_p2p.hpp): per batch parity, one byte per owned row
+    // (entity rows then feature rows, pmA / pmW words of 4) -- bit p: peer p's examples of that
+    // batch read the row (bit rank: this rank's own); a byte != 0: the batch updates the row
+    int pipe;
+    uint32_t* pm;
+    int pmA, pmW;
     // private rows: rows a single record of the global batch references (rae.h RAE_PRIV_AUTO;
     // single-rank SP plans), updated per example by the update launch's leading workgroups;
     // pmask per slot and example = (entity-slot bits j < 32, j >= 32, feature-position bits,

@@ -17,6 +17,7 @@
 #pragma once
 #include "rae_common.hpp"
 #include "rae_index.hpp"
+#include "rae_p2p.hpp"
 #include "rae_step.hpp"
 
 namespace rae {
@@ -406,11 +407,14 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
     }
 }
 
+// (pipelined peer-to-peer form: the new Ab also into the peers that read row e next batch)
 template <int OPT>
 __device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, float aab0, float gb) {
     float ac = aab0;
-    a.Ab[e] = opt_update<OPT>(ab0, &ac, gb, a.lr);
+    const float v = opt_update<OPT>(ab0, &ac, gb, a.lr);
+    a.Ab[e] = v;
     if (OPT == 0) a.aAb[e] = ac;
+    pipe_push_ab(a, e, v);
 }
 
 template <int OPT, bool V4, int Q, int VS>
@@ -462,6 +466,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
         gb = wave_sum(gb);
     }
     apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+    pipe_push_row(a, 0, e, pv.v, nv, lane);
     if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb);
 }
 
@@ -518,6 +523,7 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
             return;
         }
         apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
+        pipe_push_row(a, 0, e, pv.v, nv, lane);
         if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gt);
     }
 }
@@ -589,6 +595,7 @@ __device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<
     } else {
         float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
         apply_row<OPT, V4, Q>(a.W + (int64_t)f * m, arow, pv, av, g, nv, a.lr, lane);
+        pipe_push_row(a, 1, f, pv.v, nv, lane);
     }
 }
 
@@ -731,6 +738,7 @@ __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
     }
     if (isA) {
         apply_row<OPT, V4, Q>(prow, arow, pv, av, gs, nv, a.lr, lane);
+        pipe_push_row(a, 0, row, pv.v, nv, lane);
         if (lane == 0) ab_update<OPT>(a, row, ab0, aab0, gb);
     } else {
         feature_finish<OPT, V4, Q>(a, row, pv, av, gs, lane);

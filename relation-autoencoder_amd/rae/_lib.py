@@ -77,7 +77,7 @@ EXPORTS = (
     "rae_dp_block_floats", "rae_set_dp_buffers", "rae_dp_list_max", "rae_dp_pack",
     "rae_dp_unpack", "rae_dp_pack_at", "rae_dp_unpack_at",
     "rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_p2p_signals", "rae_set_peer",
-    "rae_set_p2p_timeout",
+    "rae_set_p2p_timeout", "rae_p2p_prologue",
 )
 RAE_IPC_HANDLE_BYTES = 64
 
@@ -107,7 +107,7 @@ KERNEL_FORMS = {
     "priv_rows": {"auto": 0, "off": 1, "on": 2},
     "dp_dense": {"auto": 0, "records": 1, "partials": 2},
     "heavy_chunk": {"auto": 0, "off": 1, "on": 2},
-    "dp_xchg": {"collective": 0, "p2p": 1},
+    "dp_xchg": {"collective": 0, "p2p": 1, "p2p_pipe": 2},
 }
 
 
@@ -173,8 +173,9 @@ def load(path: str | None = None):
     lib.rae_p2p_signals.restype = _P
     lib.rae_set_peer.argtypes = [_P, C.c_int32, _P, _P, _P, _P, _P]
     lib.rae_set_p2p_timeout.argtypes = [_P, C.c_double]
+    lib.rae_p2p_prologue.argtypes = [_P, C.c_int64, C.c_int32, _P]
     for fn in ("rae_ipc_export", "rae_ipc_open", "rae_ipc_close", "rae_set_peer",
-               "rae_set_p2p_timeout"):
+               "rae_set_p2p_timeout", "rae_p2p_prologue"):
         getattr(lib, fn).restype = C.c_int
     lib.rae_set_negatives.argtypes = [_P, _P, _P, C.c_int32, C.c_int64]
     lib.rae_set_cursor.argtypes = [_P, C.c_int64, _P]

@@ -138,9 +138,17 @@ class TrainEngine:
             raise ValueError("the partitioned data-parallel update needs the ranks' Exchange")
         # peer-to-peer exchange (include/rae.h RAE_XCHG_P2P): the kernels store rows and
         # records straight into the peers' IPC-mapped buffers -- no collective inside a step
-        self._p2p = self.kernel_forms.get("dp_xchg") == "p2p" and self.world_size > 1
-        if self.kernel_forms.get("dp_xchg") == "p2p" and self.kernel_forms["dp_update"] != "partitioned":
+        xchg = self.kernel_forms.get("dp_xchg", "collective")
+        self._p2p = xchg != "collective" and self.world_size > 1
+        if xchg != "collective" and self.kernel_forms["dp_update"] != "partitioned":
             raise ValueError("the peer-to-peer exchange runs the partitioned update")
+        # pipelined form (RAE_XCHG_P2P_PIPE): every step pushes the NEXT batch's rows, so a
+        # step needs the row lists of its batch + 1 (run() builds one batch past each window)
+        # and a run whose first batch the previous step did not push starts with
+        # rae_p2p_prologue (_p2p_start)
+        self._pipe = self._p2p and xchg == "p2p_pipe"
+        self._p2p_next = None        # batch the last queued step pushed rows for (signal out)
+        self._p2p_valid = False      # ... pushed from the current negatives' lists
         self._ipc_bases = {}         # handle bytes -> this process's mapping of a peer allocation
         # ranks on different GPUs: the kernels' xGMI stores into a peer's memory (rae_p2p.hpp
         # "Visibility across GPUs") have run on ranks sharing one GPU only -- opt-in
@@ -214,6 +222,11 @@ class TrainEngine:
         # right before its steps.
         self.index_overlap = bool(index_overlap) and self.index_window >= 2
         self._win = self.index_window // 2 if self.index_overlap else self.index_window
+        # pipelined p2p: each window's index covers one batch more (the last step's next
+        # batch), so the ring holds a window + 1 beside the next window's build
+        self._look = 1 if self._pipe else 0
+        if self._look:
+            self._win = max(1, self._win - 1)
         self._idx_stream = None
         if self.index_overlap:
             lo, _ = torch.cuda.Stream.priority_range()
@@ -631,7 +644,9 @@ class TrainEngine:
         wins = self.windows(first_batch, count)
         for wi, (b, n) in enumerate(wins):
             if index:
-                self._index_ready(b, n)
+                self._index_ready(b, min(n + self._look, self.nb - b))
+            if wi == 0 and self._pipe:
+                self._p2p_start(b)
             nn_ = 0
             if pre:
                 nn_ = wins[wi + 1][1] if wi + 1 < len(wins) else min(n, self.nb - (b + n))
@@ -646,7 +661,19 @@ class TrainEngine:
                 gate.record(torch.cuda.current_stream(self.device))
             self._queue_window(b, n, wi, replays, graph)
             if gate is not None:
-                self.prefetch_index(b + n, nn_, after=gate)
+                self.prefetch_index(b + n, min(nn_ + self._look, self.nb - (b + n)), after=gate)
+        if self._pipe and count > 0:
+            # the run's last step pushed (and signalled) the rows of the batch after it
+            self._p2p_next, self._p2p_valid = first_batch + count, True
+
+    def _p2p_start(self, b: int):
+        """Pipelined p2p: unless the previous step already pushed batch b's rows (from the
+        current negatives' lists), push them now -- after consuming that step's signal for
+        another batch (every rank runs the same batches, so every rank decides alike)."""
+        if self._p2p_valid and self._p2p_next == b:
+            return
+        _lib.check(self.lib.rae_p2p_prologue(self.plan, int(b), 1 if self._p2p_next is not None else 0,
+                                             self._stream()), "rae_p2p_prologue")
 
     def _queue_window(self, b, n, wi, replays, graph):
         """Queue the steps of window [b, b+n) (graph replays or eager launches)."""
@@ -740,6 +767,7 @@ class TrainEngine:
     def _new_negatives(self):
         self._drain_prefetch()
         self._neg_version += 1
+        self._p2p_valid = False      # rows pushed from the old lists: push the next run's again
 
     # ------------------------------------------------------------------ labelling
     def label(self, split: DeviceSplit, row0: int, nrows: int, probs: bool = True):

@@ -224,8 +224,8 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", ind
                                                priv_rows=priv, dp_xchg=xchg),
                              index_window=index_window)
     ind.learn(verbose=False)
-    if xchg == "p2p":
-        assert ind.engine.kernel_forms_in_use()["dp_xchg"] == "p2p"
+    if xchg != "collective":
+        assert ind.engine.kernel_forms_in_use()["dp_xchg"] == xchg
     if decoder == "sp" and dense != "auto":
         assert ind.engine.kernel_forms_in_use()["dp_dense"] == dense
     if priv != "auto":
@@ -280,8 +280,8 @@ def c4dp_dataset():
 
 def run_gpu_c4dp(out, dp_update="replicated"):
     xchg = "collective"
-    if dp_update == "p2p":               # the partitioned update over the peer-to-peer exchange
-        dp_update, xchg = "partitioned", "p2p"
+    if dp_update in ("p2p", "p2p_pipe"):   # the partitioned update over a peer-to-peer exchange
+        dp_update, xchg = "partitioned", dp_update
     """BASELINE config 4's model shape (K = 300, embed 300, neg 50, l = 100 per rank) on a
     reduced synthetic set: the data-parallel kernels the 8-GPU config runs together -- the split
     SP forward (r m > 32768), the wire records with every example's dw1 / dw2 (dp_dense records
@@ -314,7 +314,7 @@ def run_gpu_c4dp(out, dp_update="replicated"):
         eng.sync_replicas()
         for k, v in ind.modelFunc.named_params().items():
             snap[f"{k}@{b}"] = v.detach().cpu().numpy()
-    np.savez(os.path.join(out, f"c4dp_{dp_update if xchg == 'collective' else 'p2p'}_{rk}.npz"),
+    np.savez(os.path.join(out, f"c4dp_{dp_update if xchg == 'collective' else xchg}_{rk}.npz"),
              costs=eng.costs[:c["steps"]].cpu().numpy(), **snap)
 
 

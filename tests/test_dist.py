@@ -160,7 +160,7 @@ def test_gpu_partitioned_update(built_lib, cuda_dev, tmp_path, decoder, ws, dens
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("xchg", ["collective", "p2p"])
+@pytest.mark.parametrize("xchg", ["collective", "p2p", "p2p_pipe"])
 def test_gpu_partitioned_large_vocabulary(built_lib, cuda_dev, tmp_path, xchg):
     """vocabularies whose owned rows exceed the row lists' LDS bitmap take
     k_build_dplists' hash passes (sized from the owned candidates, restarted with more passes
@@ -174,7 +174,7 @@ def test_gpu_partitioned_large_vocabulary(built_lib, cuda_dev, tmp_path, xchg):
     _launch(["gpu", str(tmp_path), "sp", "partitioned", "auto", "auto", "0", xchg, "1", "big"])
     _launch(["gpu", str(tmp_path), "sp", "replicated", "auto", "auto", "0", "collective", "1",
              "big"])
-    tag = "partitioned" if xchg == "collective" else "partitioned_p2p"
+    tag = "partitioned" if xchg == "collective" else f"partitioned_{xchg}"
     gp = [np.load(tmp_path / f"gpu_{tag}_big_sp_{k}.npz") for k in range(2)]
     gr = np.load(tmp_path / "gpu_replicated_big_sp_0.npz")
     for k in gr.files:
@@ -270,10 +270,12 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
     _launch(["gpu_c4dp", str(tmp_path), "replicated"], nproc=ws, timeout=600)
     _launch(["gpu_c4dp", str(tmp_path), "partitioned"], nproc=ws, timeout=600)
     _launch(["gpu_c4dp", str(tmp_path), "p2p"], nproc=ws, timeout=600)
+    _launch(["gpu_c4dp", str(tmp_path), "p2p_pipe"], nproc=ws, timeout=600)
     want_c, want_p, (single_p, single_c) = _c4dp_reference(cuda_dev, ws)
     gr = [np.load(tmp_path / f"c4dp_replicated_{k}.npz") for k in range(ws)]
     gp = [np.load(tmp_path / f"c4dp_partitioned_{k}.npz") for k in range(ws)] + \
-        [np.load(tmp_path / f"c4dp_p2p_{k}.npz") for k in range(ws)]
+        [np.load(tmp_path / f"c4dp_p2p_{k}.npz") for k in range(ws)] + \
+        [np.load(tmp_path / f"c4dp_p2p_pipe_{k}.npz") for k in range(ws)]
     last = C4DP_SHAPE["steps"] - 1
     for g in gr[1:] + gp:
         np.testing.assert_array_equal(g["costs"], gr[0]["costs"])
@@ -289,10 +291,13 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("decoder,ws,graph_chunk,iw", [("sp", 2, 1, 0), ("sp", 4, 4, 0),
-                                                       ("rescal", 2, 1, 0), ("rescal+sp", 4, 1, 0),
-                                                       ("sp", 8, 4, 0), ("sp", 2, 2, 4)])
-def test_gpu_p2p_exchange(built_lib, cuda_dev, tmp_path, decoder, ws, graph_chunk, iw):
+@pytest.mark.parametrize("decoder,ws,graph_chunk,iw,xchg", [
+    ("sp", 2, 1, 0, "p2p"), ("sp", 4, 4, 0, "p2p"), ("rescal", 2, 1, 0, "p2p"),
+    ("rescal+sp", 4, 1, 0, "p2p"), ("sp", 8, 4, 0, "p2p"), ("sp", 2, 2, 4, "p2p"),
+    ("sp", 2, 1, 0, "p2p_pipe"), ("sp", 4, 4, 0, "p2p_pipe"), ("rescal", 2, 1, 0, "p2p_pipe"),
+    ("rescal+sp", 4, 1, 0, "p2p_pipe"), ("sp", 8, 4, 0, "p2p_pipe"), ("sp", 2, 2, 4, "p2p_pipe"),
+    ("sp", 2, 4, 6, "p2p_pipe")])
+def test_gpu_p2p_exchange(built_lib, cuda_dev, tmp_path, decoder, ws, graph_chunk, iw, xchg):
     """the partitioned update over the peer-to-peer exchange (include/rae.h
     RAE_XCHG_P2P, csrc/rae_p2p.hpp) -- owners store the rows each peer's next batch reads into
     the peer's IPC-mapped replica, every forward stores its records into every peer's exchange
@@ -300,12 +305,16 @@ def test_gpu_p2p_exchange(built_lib, cuda_dev, tmp_path, decoder, ws, graph_chun
     sharing the GPU, eager (graph_chunk 1) and graph-replayed (no collective inside a step, so
     the steps capture under gloo too), iw = 4: a ring of four batches (many windows, the row-list
     capacities agreed per window).  == the collective replicated update bitwise (costs and
-    parameters), replicas bit-identical after the final gather, == the float64 oracle."""
-    _launch(["gpu", str(tmp_path), decoder, "partitioned", "auto", "auto", str(iw), "p2p",
+    parameters), replicas bit-identical after the final gather, == the float64 oracle.
+    p2p_pipe (RAE_XCHG_P2P_PIPE): the next batch's rows leave during the step -- those the
+    update leaves unchanged right after the forward, the updated ones from the row tasks --
+    with the lookahead of one batch past every window (ring of 4 / 6: windows of one and two
+    batches, the next window's index built beside the steps) and a prologue per epoch."""
+    _launch(["gpu", str(tmp_path), decoder, "partitioned", "auto", "auto", str(iw), xchg,
              str(graph_chunk)], nproc=ws, timeout=420)
     _launch(["gpu", str(tmp_path), decoder, "replicated", "auto", "auto", str(iw)], nproc=ws)
     tr, costs = _single_process_oracle(decoder, ws=ws)
-    gp = [np.load(tmp_path / f"gpu_partitioned_p2p_{decoder}_{k}.npz") for k in range(ws)]
+    gp = [np.load(tmp_path / f"gpu_partitioned_{xchg}_{decoder}_{k}.npz") for k in range(ws)]
     gr = np.load(tmp_path / f"gpu_replicated_{decoder}_0.npz")
     np.testing.assert_array_equal(gp[0]["costs"], gr["costs"])
     np.testing.assert_allclose(gp[0]["costs"], costs, rtol=2e-5, atol=2e-5)

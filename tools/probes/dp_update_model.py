@@ -10,6 +10,8 @@ Times, per step, with the kernels' own dispatch timestamps (rae_time_next):
   replicated   rank 0 of a G-rank plan: forward (l examples), update over the global batch
                L = G*l (with the SP wire record: k_vrec + k_update), row index of the global batch;
   partitioned  the same with the row-owner partitioned update: + the row pull's pack / unpack.
+  p2p_pipe     the same with the next batch's rows pushed during the step (RAE_XCHG_P2P_PIPE):
+               the rows' link time is credited as hidden under the update (project_p2p_pipe);
   p2p          the partitioned update over the peer-to-peer exchange (include/rae.h RAE_XCHG_P2P):
                the row and record pushes and the signal waits are kernels of the step; here the
                "peers" are local dummy buffers and the signal words loop back to this rank's own
@@ -80,10 +82,11 @@ def measure(args, cfg, data, gold, G, mode):
     from rae.inducer import ReconstructInducer
     dev = torch.device("cuda", 0)
     forms = dict(kv.split("=", 1) for kv in args.kernel_form) if G > 1 else {}
-    p2p = mode == "p2p"
+    p2p = mode in ("p2p", "p2p_pipe")
+    pipe = mode == "p2p_pipe"
     if p2p:
+        forms["dp_xchg"] = mode
         mode = "partitioned"
-        forms["dp_xchg"] = "p2p"
         E.TrainEngine._p2p_setup = loopback_p2p_setup
     ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, args.l, cfg["r"],
                              cfg["m"], cfg["s"], 0.0, 0.0, "adagrad", "dpm", cfg["dec"], False,
@@ -105,11 +108,13 @@ def measure(args, cfg, data, gold, G, mode):
     ie[1].record(st0)
     torch.cuda.synchronize()
     index_us = ie[0].elapsed_time(ie[1]) * 1e3 / nw
-    n = min(args.iters, eng.nb, eng.index_window)
-    eng.build_index(0, n)
+    n = min(args.iters, eng.nb - eng._look, eng.index_window - eng._look)
+    eng.build_index(0, n + eng._look)
     eng.set_cursor(0)
     lib, plan = eng.lib, eng.plan
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if pipe:                               # the first step's rows (no previous step pushed them)
+        assert lib.rae_p2p_prologue(plan, 0, 0, st) == 0, lib.rae_last_error()
 
     def ev():
         h = C.c_void_p()
@@ -132,6 +137,8 @@ def measure(args, cfg, data, gold, G, mode):
         assert lib.rae_time_next(plan, *e["update"]) == 0
         assert lib.rae_step_update(plan, i, st) == 0
         evs.append(e)
+    if pipe:                               # the last step signalled batch n's rows (engine state)
+        eng._p2p_next, eng._p2p_valid = n, True
     torch.cuda.synchronize()
     for e in evs:
         for k in t:
@@ -148,9 +155,12 @@ def measure(args, cfg, data, gold, G, mode):
         blk = int(lib.rae_dp_block_floats(C.byref(eng.cfg), ca, cw)) * 4
         out["rows_alltoall_in_bytes"] = (G - 1) * blk
         out["row_caps"] = [ca, cw]
-    if p2p:
+    if p2p and not pipe:
         out["xchg"] = "p2p (forward = row push + wait + forward + record push; update = wait + "\
                       "update)"
+    if pipe:
+        out["xchg"] = "p2p_pipe (forward = wait + forward + record push + next batch's unchanged "\
+                      "rows' push; update = wait + update with the updated rows' pushes)"
     out["kernel_forms"] = eng.kernel_forms_in_use()
     out.update(graph_steps(eng, args))
     ind._drop_engine()
@@ -161,9 +171,9 @@ def graph_steps(eng, args):
     """us per step of n graph-replayed steps, alone and with the next n batches' index built
     beside them (prefetch_index on the side stream), medians over reps."""
     import torch
-    n = min(args.graph_n, eng.index_window // 2, eng.nb // 2)
+    n = min(args.graph_n, eng.index_window // 2 - eng._look, eng.nb // 2 - eng._look)
     eng.cursor_moved()
-    eng.build_index(0, n)
+    eng.build_index(0, n + eng._look)
     eng.capture_for(0, n)
     eng.run(0, n, index=False)
     main = torch.cuda.current_stream()
@@ -179,7 +189,7 @@ def graph_steps(eng, args):
         eng._ready = None                   # force the rebuild of [n, 2n) each rep
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(main)
-        eng.prefetch_index(n, n)
+        eng.prefetch_index(n + eng._look, n)
         eng.run(0, n, index=False)
         main.wait_event(eng._ready[3])
         b.record(main)
@@ -187,6 +197,25 @@ def graph_steps(eng, args):
         ovl.append(a.elapsed_time(b) * 1e3 / n)
     return {"graph_steps_n": n, "graph_step": float(np.median(alone)),
             "graph_step_with_index": float(np.median(ovl))}
+
+
+def project_p2p_pipe(r, t1, args):
+    """The pipelined peer-to-peer step: the measured graph step (its pushes' local stores and
+    the waits' polling included) + the records' link time not hidden by their push kernel + the
+    rows' link time not hidden under the update (the next batch's rows leave from the pre-push
+    right after the forward and from the update's row tasks; the peers wait for them only at
+    their next forward) + one signal latency per exchange."""
+    bw = args.links * args.link_gbs * args.eff * 1e3          # bytes per us
+    tg = r["graph_step_with_index"]
+    rec_t = r["records_allgather_in_bytes"] / bw
+    row_t = r["rows_alltoall_in_bytes"] / bw
+    hide = r["update"]                                         # wait + update (events)
+    extra = max(0.0, rec_t - args.push_us) + max(0.0, row_t - hide) + 2 * args.p2p_lat_us
+    return {"step_us": tg + extra, "kernels_us": tg, "link_and_signal_us": extra,
+            "records_in_us": rec_t, "rows_in_us": row_t, "rows_hidden_under_us": hide,
+            "efficiency": t1 / (tg + extra), "efficiency_if_link_free": t1 / tg,
+            "model": "graph step + max(0, records bytes / rate - push_us) + max(0, rows bytes / "
+                     "rate - update us) + 2 signal latencies"}
 
 
 def project_p2p(r, t1, args):
@@ -218,6 +247,9 @@ def project(res, args):
                             "model": "step = graph-replayed step with the index built beside "
                                      "it (measured) + A2A (partitioned) + AG, every collective "
                                      "lat + bytes / inbound rate, not overlapped"}}
+    if res.get("p2p_pipe"):
+        proj["p2p_pipe"] = project_p2p_pipe(res["p2p_pipe"], t1, args)
+        proj["assumptions"]["p2p_signal_latency_us"] = args.p2p_lat_us
     if res.get("p2p"):
         proj["p2p"] = project_p2p(res["p2p"], t1, args)
         proj["assumptions"]["p2p_signal_latency_us"] = args.p2p_lat_us
@@ -248,7 +280,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--graph-n", type=int, default=64, help="steps per timed graph replay")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="replicated,partitioned,p2p")
+    ap.add_argument("--modes", default="replicated,partitioned,p2p,p2p_pipe")
     ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
                     help="kernel form of the G-rank plans (e.g. priv_rows=off)")
     ap.add_argument("--link-gbs", type=float, default=76.8,
