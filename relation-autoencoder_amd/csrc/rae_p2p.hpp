@@ -84,11 +84,13 @@ __device__ void p2p_push_records(const StepArgs& a) {
     const int64_t nrb = (n4 + blockDim.x - 1) / blockDim.x;
     if (a.pipe && (int64_t)blockIdx.x >= nrb) {
         const int64_t b = step_batch(a);
-        uint4* pm = reinterpret_cast<uint4*>(a.pm + (int64_t)((b + 1) & 1) * (a.pmA + a.pmW));
+        // (stored like the pushes, so every store of this kernel is one kind)
+        float4* pm = reinterpret_cast<float4*>(a.pm + (int64_t)((b + 1) & 1) * (a.pmA + a.pmW));
         const int64_t nw4 = (a.pmA + a.pmW) / 4;                      // pmA, pmW multiples of 4
         for (int64_t i = (blockIdx.x - nrb) * blockDim.x + threadIdx.x; i < nw4;
              i += (gridDim.x - nrb) * blockDim.x)
-            pm[i] = make_uint4(0u, 0u, 0u, 0u);
+            store_sys(pm + i, make_float4(0.f, 0.f, 0.f, 0.f));
+        p2p_stores_done();
         return;
     }
     const int64_t o4 = (int64_t)a.rank * a.l * a.lay.rec / 4;

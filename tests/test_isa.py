@@ -113,23 +113,82 @@ def test_build_is_warning_free(built_lib):
     assert "warning:" not in log, log[:2000]
 
 
-P2P_PUSHES = ("_Z10k_p2p_rowsN3rae8StepArgsE", "_Z10k_p2p_recsN3rae8StepArgsE")
+P2P_PUSHES = ("_Z10k_p2p_rowsN3rae8StepArgsE", "_Z10k_p2p_recsN3rae8StepArgsE",
+              "_Z9k_p2p_preN3rae8StepArgsEii")
 
 
-def test_p2p_pushes_store_write_through_at_system_scope(disasm):
+def _pending_store_at_end(lines):
+    """Forward dataflow over the kernel's control-flow graph: is there a path from a
+    global_store to s_endpgm with no `s_waitcnt vmcnt(0)` in between?"""
+    addrs = [a for a, _ in lines]
+    index = {a: k for k, a in enumerate(addrs)}
+    succ = []
+    for k, (a, ins) in enumerate(lines):
+        op = ins.split()[0]
+        nxt = [k + 1] if k + 1 < len(lines) else []
+        if op.startswith(("s_branch", "s_cbranch")):
+            imm = int(ins.split()[1])
+            imm = imm - 65536 if imm >= 32768 else imm
+            tgt = index.get(a + 4 + 4 * imm)
+            assert tgt is not None, ins
+            nxt = [tgt] if op == "s_branch" else nxt + [tgt]
+        elif op == "s_endpgm":
+            nxt = []
+        succ.append(nxt)
+    pending = [False] * len(lines)
+    seen = [False] * len(lines)
+    work = [0]
+    seen[0] = True
+    while work:
+        k = work.pop()
+        ins = lines[k][1]
+        out = pending[k]
+        if ins.startswith("global_store"):
+            out = True
+        elif ins.startswith("s_waitcnt") and "vmcnt(0)" in ins:
+            out = False
+        if ins.startswith("s_endpgm") and pending[k]:
+            return True
+        for j in succ[k]:
+            if not seen[j] or (out and not pending[j]):
+                seen[j] = True
+                pending[j] = pending[j] or out
+                work.append(j)
+    return False
+
+
+@pytest.fixture(scope="module")
+def disasm_addr(built_lib, tmp_path_factory):
+    d = tmp_path_factory.mktemp("isa_addr")
+    fat, co = d / "fat.bin", d / "gfx950.co"
+    subprocess.run([_tool("llvm-objcopy"), "-O", "binary", "--only-section=.hip_fatbin", LIB,
+                    str(fat)], check=True)
+    subprocess.run([_tool("clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    out = subprocess.run([_tool("llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
+                         text=True).stdout
+    funcs, cur = {}, None
+    for line in out.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = funcs.setdefault(m.group(1), [])
+            continue
+        m = re.match(r"^\t(.+?)\s*//\s*([0-9A-Fa-f]+):", line)
+        if cur is not None and m:
+            cur.append((int(m.group(2), 16), m.group(1).strip()))
+    return funcs
+
+
+def test_p2p_pushes_store_write_through_at_system_scope(disasm_addr):
     """rae_p2p.hpp "Visibility across GPUs", producer side: every store of the push kernels
-    into a peer's memory is a system-scope write-through (sc0 sc1), and the waves end only
-    through a vmcnt(0) wait -- no pushed byte is left dirty in one of this GPU's L2s, or in
-    flight, when the signal kernel that follows runs."""
+    into a peer's memory is a system-scope write-through (sc0 sc1), and no path of the kernel
+    reaches s_endpgm with a store not yet waited for (vmcnt(0)) -- no pushed byte is left dirty
+    in one of this GPU's L2s, or in flight, when the signal kernel that follows runs."""
     for name in P2P_PUSHES:
-        code = disasm.get(name)
-        assert code, f"{name} is not in the code object"
-        stores = [c for c in code if c.startswith("global_store")]
+        lines = disasm_addr.get(name)
+        assert lines, f"{name} is not in the code object"
+        stores = [c for _, c in lines if c.startswith("global_store")]
         assert stores, name
         for c in stores:
             assert re.search(r"\bsc0\b", c) and re.search(r"\bsc1\b", c), c
-        ends = [i for i, c in enumerate(code) if c.startswith("s_endpgm")]
-        assert ends, name
-        for i in ends:
-            assert code[i - 1].startswith("s_waitcnt") and "vmcnt(0)" in code[i - 1], \
-                (name, code[i - 1])
+        assert not _pending_store_at_end(lines), name
