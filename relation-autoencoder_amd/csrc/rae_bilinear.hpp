@@ -269,6 +269,9 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
 #define RAE_MT_STAMP(slot) do { } while (0)
 #endif
 
+template <int OPT>
+__device__ void mt_rblock_update(const StepArgs& a, int i, int j0, int lane);
+
 // DP: the instantiation that may carry the dP contraction (the second pass); the first pass's
 // instantiation has none of its registers (occupancy)
 template <bool BF16, bool DIRECT = false, bool DP = true>
@@ -524,6 +527,17 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
                 }
                 RAE_MT_STAMP(7);
             }
+        }
+    }
+    if constexpr (BF16 && DP) {
+        // the R update of this step (rae.h RAE_BILRUPD_MTILE), after the block's last use of
+        // its staged (pre-update) image: wave w updates R[i0 + w][j0 .. j0 + 15][:] -- k_bil_rows'
+        // gradient and optimizer arithmetic on the same rows, so R is bit-identical to the
+        // separate update's; no other workgroup reads this block in this launch
+        static_assert(RAE_MTI == RAE_MTW, "one row i of the block per wave");
+        if (dpass && a.rfuse && i0 + w < r) {
+            if (a.opt == 0) mt_rblock_update<0>(a, i0 + w, j0, lane);
+            else mt_rblock_update<1>(a, i0 + w, j0, lane);
         }
     }
 }
@@ -1281,6 +1295,51 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     const bool ijv = ij < (int64_t)r * r;
     const int ijc = (int)(ijv ? ij : 0);
     bilinear_rows_acc_bf16_ij(a, ijc / r, ijc - (ijc / r) * r, ijv, kg0, nk, acc, lane);
+}
+
+// The second M-tile pass's R update (bil_mt): rows (i, j0 .. j0 + 15) of R x all m in one
+// wave -- the gradient as k_bil_rows forms it (bilinear_rows_acc_bf16_ij: same operands, same
+// K order; one K step per round trip here, the pass's register budget), then every R and
+// optimizer-state load of the tile in one round, the optimizer, float4 stores
+template <int OPT>
+__device__ void mt_rblock_update(const StepArgs& a, int i, int j0, int lane) {
+    const int m = a.m, r = a.r;
+    const int li = lane & 15, kk = lane >> 4;
+    const int j = j0 + li;
+    const bool ijv = j < r;
+    const int nk = (m + 15) / 16;                         // <= RAE_KG (plan creation)
+    rae_bf4 acc[RAE_KG];
+#pragma unroll
+    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
+    bilinear_rows_acc_bf16_ij<false>(a, i, ijv ? j : 0, ijv, 0, nk, acc, lane);
+    const int64_t ij = (int64_t)i * r + (ijv ? j : 0);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int H = RAE_KG / 2;                         // two rounds: the pass's VGPR budget
+#pragma unroll
+    for (int h = 0; h < RAE_KG; h += H) {
+        float4 wv[H], av[H];
+#pragma unroll
+        for (int u = 0; u < H; ++u) {
+            const int q = h + u, k0 = q * 16 + 4 * kk;
+            const bool ok = q < nk && ijv && k0 < m;
+            const int64_t o = ok ? ij * m + k0 : 0;
+            wv[u] = ok ? *reinterpret_cast<const float4*>(a.R3 + o) : z4;
+            av[u] = (OPT == 0 && ok) ? *reinterpret_cast<const float4*>(a.aR3 + o) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < H; ++u) {
+            const int q = h + u, k0 = q * 16 + 4 * kk;
+            if (!(q < nk && ijv && k0 < m)) continue;
+            const int64_t o = ij * m + k0;
+            float4 w = wv[u], ac = av[u];
+            w.x = opt_update<OPT>(w.x, &ac.x, acc[q][0], a.lr);
+            w.y = opt_update<OPT>(w.y, &ac.y, acc[q][1], a.lr);
+            w.z = opt_update<OPT>(w.z, &ac.z, acc[q][2], a.lr);
+            w.w = opt_update<OPT>(w.w, &ac.w, acc[q][3], a.lr);
+            *reinterpret_cast<float4*>(a.R3 + o) = w;
+            if (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + o) = ac;
+        }
+    }
 }
 
 // One wave: 16 rows ij x all m columns.  The gradient tile comes out transposed (D[k][ij]:
