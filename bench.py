@@ -48,8 +48,11 @@ CONFIGS = {
                name="C2 synthetic 100k triples K=30 embed=100 neg=10 sp"),
     "c3": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="sp", ntrue=100,
                name="C3 synthetic 1M triples K=100 embed=200 neg=20 sp (headline)"),
+    # dp_update: the data-parallel update form --dp-update auto picks (tools/probes/
+    # dp_update_model.py, DESIGN.md 4: at G = 8, l = 100 C4 projects 31.7 % partitioned vs
+    # 27.2 % replicated over RCCL, C3 24.5 % vs 26.3 %)
     "c4": dict(N=10_000_000, d=2 ** 20, m=300, r=300, s=50, dec="sp", ntrue=300,
-               name="C4 synthetic 10M triples K=300 embed=300 neg=50 sp"),
+               dp_update="partitioned", name="C4 synthetic 10M triples K=300 embed=300 neg=50 sp"),
     "c5": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="rescal", ntrue=100, bf16=True,
                name="C5 synthetic 1M triples K=100 embed=200 neg=20 rescal, bf16 MFMA"),
 }
@@ -258,9 +261,10 @@ def main():
     ap.add_argument("--kernel-form", action="append", default=[], metavar="KEY=VALUE",
                     help="pin a kernel form (include/rae.h; e.g. sp_forward=split); recorded in "
                          "config.kernel_forms")
-    ap.add_argument("--dp-update", default="replicated", choices=["replicated", "partitioned"],
+    ap.add_argument("--dp-update", default="auto", choices=["auto", "replicated", "partitioned"],
                     help="data-parallel update (N > 1): every rank updates every row, or each "
-                         "rank the rows it owns (rows pulled from their owners each step)")
+                         "rank the rows it owns (rows pulled from their owners each step); auto: "
+                         "the config's projected better form (C4 partitioned, else replicated)")
     ap.add_argument("--dp-xchg", default="collective", choices=["collective", "p2p", "p2p_pipe"],
                     help="partitioned update, N > 1: RCCL collectives between the step launches, or "
                          "the kernels' own stores into the peers' IPC-mapped buffers (include/rae.h "
@@ -269,6 +273,8 @@ def main():
                     help="--dp-xchg p2p with ranks on different GPUs (verified on ranks sharing "
                          "one GPU only; refused without this flag)")
     args = ap.parse_args()
+    if args.dp_update == "auto":
+        args.dp_update = CONFIGS[args.config].get("dp_update", "replicated")
     if args.dp_xchg != "collective":
         args.dp_update = "partitioned"
         args.kernel_form.append(f"dp_xchg={args.dp_xchg}")

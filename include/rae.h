@@ -96,7 +96,6 @@ typedef struct rae_config {
     int32_t dp_dense;         /* data-parallel SP: dense decoder-matrix gradients RAE_DPDENSE_* */
     int32_t heavy_chunk;      /* very heavy rows split into record chunks: RAE_HCHUNK_*      */
     int32_t dp_xchg;          /* data-parallel exchange: RAE_XCHG_*                          */
-    int32_t bil_rupd;         /* bilinear R / C tensor update: RAE_BILRUPD_*                   */
 } rae_config;
 
 #define RAE_SPFWD_AUTO 0      /* fused per-example kernel unless r*m > 32768                  */
@@ -147,13 +146,6 @@ typedef struct rae_config {
                                * every updated row by the update task that writes it -- so the   *
                                * row bytes travel under the update; world_size <= 8, private     *
                                * rows off; rae_p2p_prologue before the first step of a run       */
-
-#define RAE_BILRUPD_AUTO 0    /* in the second M-tile pass when it can be (below), else separate  */
-#define RAE_BILRUPD_SEPARATE 1 /* the update launch's R tiles (k_bil_update / k_bil_rows)         */
-#define RAE_BILRUPD_MTILE 2   /* the second M-tile pass updates the R block it staged, after its  *
-                               * contractions (one rank, bf16 operands written by the forward,   *
-                               * m <= 128 and a multiple of 4, no regulariser): R is read from  *
-                               * HBM once less per step; rae_step_forward then changes R        */
 
 /* Caller-owned device buffers.  Shapes are the reference's (fp32 everywhere):
  *   W (d,m)  Wb (m)  A (n,r)  Ab (n)  C1,C2 (r,m)  R (r,r,m) [rescal] / C (r,r,m) [hybrid]

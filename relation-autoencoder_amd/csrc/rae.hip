@@ -99,13 +99,11 @@ __global__ __launch_bounds__(RAE_FBT) void k_bil_enc_fast(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bil_encode_fast<D>(a, step_batch(a), blockIdx.x, smem);
 }
-// occupancy target of the M-tile passes (waves per SIMD): 4 keeps two 8-wave blocks per CU
-// (<= 128 VGPRs) -- the second pass with the fused R update would otherwise take 131 and run
-// one block per CU (325 blocks: two rounds)
-#ifndef RAE_MT_WPE
-#define RAE_MT_WPE 4
-#endif
+#ifdef RAE_MT_WPE      // A/B: occupancy target of the M-tile passes (waves per SIMD)
 #define RAE_MT_ATTR __attribute__((amdgpu_waves_per_eu(RAE_MT_WPE)))
+#else
+#define RAE_MT_ATTR
+#endif
 template <bool BF16, bool DIRECT = false, bool DP = true>
 __global__ __launch_bounds__(RAE_MTT) RAE_MT_ATTR void k_bil_mt(StepArgs a, int pass) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -707,10 +705,9 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
         c.priv_rows < RAE_PRIV_AUTO || c.priv_rows > RAE_PRIV_ON ||
         c.dp_dense < RAE_DPDENSE_AUTO || c.dp_dense > RAE_DPDENSE_PARTIALS ||
         c.heavy_chunk < RAE_HCHUNK_AUTO || c.heavy_chunk > RAE_HCHUNK_ON ||
-        c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P_PIPE ||
-        c.bil_rupd < RAE_BILRUPD_AUTO || c.bil_rupd > RAE_BILRUPD_MTILE)
+        c.dp_xchg < RAE_XCHG_COLLECTIVE || c.dp_xchg > RAE_XCHG_P2P_PIPE)
         return fail(RAE_E_INVALID, "unknown kernel form (sp_forward / bil_dp / bil_prep / dp_update / "
-                                   "priv_rows / dp_dense / heavy_chunk / dp_xchg / bil_rupd)");
+                                   "priv_rows / dp_dense / heavy_chunk / dp_xchg)");
     if (c.dp_xchg != RAE_XCHG_COLLECTIVE &&
         (c.dp_update != RAE_DPUPD_PARTITIONED || c.world_size > 31 || c.embed % 4 ||
          c.relations % 4 || c.embed > 512 || c.relations > 512))
@@ -970,18 +967,6 @@ extern "C" int rae_plan_create(const rae_config* cfg, const rae_buffers* buf, ra
     const size_t o_pmask = a.priv ? take(16ull * W_ * L) : 0;
     a.Lp = (L + 31) / 32 * 32;
     a.fuse_prep = (a.bf16 && c.world_size == 1 && c.bil_prep == RAE_BILPREP_AUTO) ? 1 : 0;
-    // the R update inside the second M-tile pass: the pass has the batch's R-gradient operands
-    // (written by the forward itself, fuse_prep) and its own R block; per wave one row i of the
-    // block x its 16 columns j (RAE_MTI == waves), one 16-column group of m per MFMA tile
-    const bool rfuse_ok = mtdp && a.fuse_prep && !a.reg_on && c.relations % 4 == 0 &&
-                          (c.relations + 15) / 16 <= RAE_KG;
-    if (c.bil_rupd == RAE_BILRUPD_MTILE && !rfuse_ok) {
-        delete p;
-        return fail(RAE_E_INVALID, "bil_rupd MTILE needs a single-rank bf16 bilinear plan with the "
-                                   "M-tile dP contraction, no regulariser, relations a multiple of 4 "
-                                   "up to 128");
-    }
-    a.rfuse = (rfuse_ok && c.bil_rupd != RAE_BILRUPD_SEPARATE) ? 1 : 0;
     const size_t o_fac = a.bf16 ? take(16ull * c.embed * a.Lp) : 0;
     const size_t o_vb = a.lay.wire ? take(4ull * a.vbs * L) : 0;
     const size_t o_dwb = a.dpart ? take(4ull * a.dws * L) : 0;
@@ -1156,7 +1141,6 @@ extern "C" int rae_plan_forms(const rae_plan* p, rae_config* out) {
                   : (p->args.lay.wire == 1 ? RAE_DPDENSE_RECORDS : 0);
     out->heavy_chunk = p->args.hch ? RAE_HCHUNK_ON : RAE_HCHUNK_OFF;
     out->dp_xchg = p->cfg.dp_xchg;
-    out->bil_rupd = !bil ? 0 : (p->args.rfuse ? RAE_BILRUPD_MTILE : RAE_BILRUPD_SEPARATE);
     return RAE_OK;
 }
 
@@ -1324,11 +1308,6 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         if (a.bf16 && !a.fuse_prep) {
             const int gp = 4 * ((a.r + 63) / 64) * (a.Lp / 32) + (a.Lp / 32) * ((a.m + 15) / 16);
             RAE_LAUNCH(p, k_bil_prep, dim3(gp), bt, 0, st, a);
-        }
-        if (a.rfuse) {        // R was updated by the second M-tile pass (rae_bilinear.hpp)
-            if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
-            else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
-            return;
         }
         const int nRt = n_rtiles(a.dec, a.r, a.m);
         const dim3 gr((nRt + RAE_NWAVE - 1) / RAE_NWAVE);

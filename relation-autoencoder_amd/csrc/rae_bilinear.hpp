@@ -269,9 +269,6 @@ __host__ __device__ inline size_t bil_mt_lds_bytes(int m, bool bf16) {
 #define RAE_MT_STAMP(slot) do { } while (0)
 #endif
 
-template <int OPT>
-__device__ void mt_rblock_update(const StepArgs& a, int i, int j0, int lane);
-
 // DP: the instantiation that may carry the dP contraction (the second pass); the first pass's
 // instantiation has none of its registers (occupancy)
 template <bool BF16, bool DIRECT = false, bool DP = true>
@@ -529,17 +526,6 @@ __device__ void bil_mt(const StepArgs& a, int pass, char* smem) {
             }
         }
     }
-    if constexpr (BF16 && DP) {
-        // the R update of this step (rae.h RAE_BILRUPD_MTILE), after the block's last use of
-        // its staged (pre-update) image: wave w updates R[i0 + w][j0 .. j0 + 15][:] -- k_bil_rows'
-        // gradient and optimizer arithmetic on the same rows, so R is bit-identical to the
-        // separate update's; no other workgroup reads this block in this launch
-        static_assert(RAE_MTI == RAE_MTW, "one row i of the block per wave");
-        if (dpass && a.rfuse && i0 + w < r) {
-            if (a.opt == 0) mt_rblock_update<0>(a, i0 + w, j0, lane);
-            else mt_rblock_update<1>(a, i0 + w, j0, lane);
-        }
-    }
 }
 
 // sum of the per-block partials [q0, q1) of one example's M-tile output (four interleaved
@@ -558,34 +544,6 @@ __device__ __forceinline__ float mt_sum(const float* part, int q0, int q1, int l
     for (; q < q1; ++q) t0 += p[q * st];
     return (t0 + t1) + (t2 + t3);
 }
-// the same sum with every partial's load issued at once (q1 - q0 <= NMAX; q0 is a valid block
-// index): one memory round trip instead of one per four partials, and exactly mt_sum's adds
-// in mt_sum's order -- chains t0..t3 over the full groups of four, the rest into t0
-template <int NMAX>
-__device__ __forceinline__ float mt_sum_1rt(const float* part, int q0, int q1, int l, int r4, int b, int i) {
-    const int n = q1 - q0;
-    if (n > NMAX) return mt_sum(part, q0, q1, l, r4, b, i);
-    const float* p = part + (int64_t)b * r4 + i;
-    const int64_t st = (int64_t)l * r4;
-    float v[NMAX];
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u) v[u] = p[(int64_t)(q0 + (u < n ? u : 0)) * st];
-    const int nf = n & ~3;
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-#pragma unroll
-    for (int u = 0; u < NMAX; u += 4) {
-        if (u < nf) {
-            t0 += v[u];
-            t1 += v[u + 1];
-            t2 += v[u + 2];
-            t3 += v[u + 3];
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < NMAX; ++u)
-        if (u >= nf && u < n) t0 += v[u];
-    return (t0 + t1) + (t2 + t3);
-}
 // One example's M-tile sums with four threads per element i: quarter qd of the workgroup's
 // index space sums half the partials of one output -- qd 0/1: the j-block partials (mtV),
 // qd 2/3: the i-block partials (mtW) -- into q0v / q1v / q0w / q1w; the caller combines the
@@ -598,8 +556,8 @@ __device__ __forceinline__ void mt_sums_split(const StepArgs& a, int b, float* q
     for (int e = threadIdx.x; e < 4 * r4; e += T) {
         const int qd = e / r4, i = e - qd * r4;
         const int n = qd < 2 ? nbj : nbi, h = n / 2;
-        const float t = i < r ? mt_sum_1rt<16>(qd < 2 ? a.mtV : a.mtW, (qd & 1) ? h : 0,
-                                               (qd & 1) ? n : h, a.l, r4, b, i) : 0.f;
+        const float t = i < r ? mt_sum(qd < 2 ? a.mtV : a.mtW, (qd & 1) ? h : 0, (qd & 1) ? n : h,
+                                       a.l, r4, b, i) : 0.f;
         (qd == 0 ? q0v : qd == 1 ? q1v : qd == 2 ? q0w : q1w)[i] = t;
     }
 }
@@ -1072,7 +1030,6 @@ __device__ void bil_gemm_dp(const StepArgs& a, int t, int lane) {
 // thread has ~nib / NS independent loads instead of nib.
 #define RAE_FINT 1024
 #define RAE_FINW (RAE_FINT / RAE_WAVE)
-#define RAE_FIN_Q 40     // dP partials per split summed from one round of loads
 __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, float* red) {
     const int m = a.m, r = a.r, l = a.l;
     const bool hybrid = a.dec == 2;
@@ -1088,26 +1045,14 @@ __device__ void bil_finish(const StepArgs& a, int bl, float* sdp, float* smt, fl
         const int sp = e / m, k = e - sp * m;
         const float* pp = pbase + (int64_t)bl * m + k;
         const int64_t st = (int64_t)l * m;
-        // eight independent chains, fixed order: chain u sums partials sp + NS q, q = u mod 8,
-        // in increasing q.  Up to RAE_FIN_Q partials per split: every load issued at once (one
-        // round trip, clamped addresses), then the adds in that order
+        // eight independent chains (fixed order): the loads of eight partials issue together
         float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        const int nper = sp < npart ? (npart - sp + NS - 1) / NS : 0;
-        if (nper <= RAE_FIN_Q) {
-            float v[RAE_FIN_Q];
+        int ib = sp;
+        for (; ib + 7 * NS < npart; ib += 8 * NS) {
 #pragma unroll
-            for (int q = 0; q < RAE_FIN_Q; ++q) v[q] = pp[(int64_t)(q < nper ? sp + q * NS : 0) * st];
-#pragma unroll
-            for (int q = 0; q < RAE_FIN_Q; ++q)
-                if (q < nper) t[q & 7] += v[q];
-        } else {
-            int ib = sp;
-            for (; ib + 7 * NS < npart; ib += 8 * NS) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) t[u] += pp[(ib + u * NS) * st];
-            }
-            for (int u = 0; ib < npart; ib += NS, ++u) t[u] += pp[ib * st];
+            for (int u = 0; u < 8; ++u) t[u] += pp[(ib + u * NS) * st];
         }
+        for (int u = 0; ib < npart; ib += NS, ++u) t[u] += pp[ib * st];
         sdp[e] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
     mt_sums_split<RAE_FINT>(a, bl, smt, smt + 1024, smt + 2048, smt + 3072);
@@ -1295,51 +1240,6 @@ __device__ __forceinline__ void bilinear_rows_acc_bf16(const StepArgs& a, int ij
     const bool ijv = ij < (int64_t)r * r;
     const int ijc = (int)(ijv ? ij : 0);
     bilinear_rows_acc_bf16_ij(a, ijc / r, ijc - (ijc / r) * r, ijv, kg0, nk, acc, lane);
-}
-
-// The second M-tile pass's R update (bil_mt): rows (i, j0 .. j0 + 15) of R x all m in one
-// wave -- the gradient as k_bil_rows forms it (bilinear_rows_acc_bf16_ij: same operands, same
-// K order; one K step per round trip here, the pass's register budget), then every R and
-// optimizer-state load of the tile in one round, the optimizer, float4 stores
-template <int OPT>
-__device__ void mt_rblock_update(const StepArgs& a, int i, int j0, int lane) {
-    const int m = a.m, r = a.r;
-    const int li = lane & 15, kk = lane >> 4;
-    const int j = j0 + li;
-    const bool ijv = j < r;
-    const int nk = (m + 15) / 16;                         // <= RAE_KG (plan creation)
-    rae_bf4 acc[RAE_KG];
-#pragma unroll
-    for (int q = 0; q < RAE_KG; ++q) acc[q] = rae_bf4{0.f, 0.f, 0.f, 0.f};
-    bilinear_rows_acc_bf16_ij<false>(a, i, ijv ? j : 0, ijv, 0, nk, acc, lane);
-    const int64_t ij = (int64_t)i * r + (ijv ? j : 0);
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    constexpr int H = RAE_KG / 2;                         // two rounds: the pass's VGPR budget
-#pragma unroll
-    for (int h = 0; h < RAE_KG; h += H) {
-        float4 wv[H], av[H];
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-            const int q = h + u, k0 = q * 16 + 4 * kk;
-            const bool ok = q < nk && ijv && k0 < m;
-            const int64_t o = ok ? ij * m + k0 : 0;
-            wv[u] = ok ? *reinterpret_cast<const float4*>(a.R3 + o) : z4;
-            av[u] = (OPT == 0 && ok) ? *reinterpret_cast<const float4*>(a.aR3 + o) : z4;
-        }
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-            const int q = h + u, k0 = q * 16 + 4 * kk;
-            if (!(q < nk && ijv && k0 < m)) continue;
-            const int64_t o = ij * m + k0;
-            float4 w = wv[u], ac = av[u];
-            w.x = opt_update<OPT>(w.x, &ac.x, acc[q][0], a.lr);
-            w.y = opt_update<OPT>(w.y, &ac.y, acc[q][1], a.lr);
-            w.z = opt_update<OPT>(w.z, &ac.z, acc[q][2], a.lr);
-            w.w = opt_update<OPT>(w.w, &ac.w, acc[q][3], a.lr);
-            *reinterpret_cast<float4*>(a.R3 + o) = w;
-            if (OPT == 0) *reinterpret_cast<float4*>(a.aR3 + o) = ac;
-        }
-    }
 }
 
 // One wave: 16 rows ij x all m columns.  The gradient tile comes out transposed (D[k][ij]:

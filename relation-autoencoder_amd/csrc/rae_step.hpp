@@ -193,7 +193,6 @@ struct StepArgs {
     float* facT;
     uint4* pfrag;
     int Lp;
-    int rfuse;           // the second M-tile pass updates its staged R block (rae.h RAE_BILRUPD_MTILE)
     int fuse_prep;       // single rank: the forward kernels write facT / pfrag themselves (no
                          // k_bil_prep launch); padding (b >= L, k >= m) stays zero from creation
     double* regpart;     // [nreg][2] L1/L2 partials of regularised rows

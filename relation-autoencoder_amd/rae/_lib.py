@@ -94,7 +94,7 @@ class RaeConfig(C.Structure):
         ("index_window", C.c_int64), ("mfma_bf16", C.c_int32),
         ("sp_forward", C.c_int32), ("bil_dp", C.c_int32), ("bil_prep", C.c_int32),
         ("dp_update", C.c_int32), ("priv_rows", C.c_int32), ("dp_dense", C.c_int32),
-        ("heavy_chunk", C.c_int32), ("dp_xchg", C.c_int32), ("bil_rupd", C.c_int32),
+        ("heavy_chunk", C.c_int32), ("dp_xchg", C.c_int32),
     ]
 
 
@@ -108,7 +108,6 @@ KERNEL_FORMS = {
     "dp_dense": {"auto": 0, "records": 1, "partials": 2},
     "heavy_chunk": {"auto": 0, "off": 1, "on": 2},
     "dp_xchg": {"collective": 0, "p2p": 1, "p2p_pipe": 2},
-    "bil_rupd": {"auto": 0, "separate": 1, "mtile": 2},
 }
 
 

@@ -375,9 +375,7 @@ class TrainEngine:
         batch references updated per example, or by the row tasks), dp_dense records|partials
         (data-parallel SP: dw1 / dw2 per example in the exchange, or each rank's reduced dense
         gradients), heavy_chunk off|on (rows with at least 256 records of the global batch
-        summed as parallel 128-record chunks), bil_rupd separate|mtile (bilinear: the R tensor
-        updated by the update launch, or by the second M-tile pass right after its
-        contractions).  Keys of forms that do not apply to the plan are left out."""
+        summed as parallel 128-record chunks).  Keys of forms that do not apply to the plan are left out."""
         out = _lib.RaeConfig()
         _lib.check(self.lib.rae_plan_forms(self.plan, C.byref(out)), "rae_plan_forms")
         F = _lib.KERNEL_FORMS
@@ -390,7 +388,6 @@ class TrainEngine:
             res["bil_dp"] = name["bil_dp"][out.bil_dp]
             if self.cfg.mfma_bf16:
                 res["bil_prep"] = name["bil_prep"][out.bil_prep]
-            res["bil_rupd"] = name["bil_rupd"][out.bil_rupd]
         res["dp_update"] = name["dp_update"][out.dp_update]
         res["priv_rows"] = name["priv_rows"][out.priv_rows]
         if sp and self.world_size > 1:

@@ -367,41 +367,6 @@ def test_bf16_bilinear_bitwise_deterministic(built_lib, cuda_dev, dec):
         assert np.array_equal(out[0][0][k], out[1][0][k]), k
 
 
-@pytest.mark.parametrize("dec,opt", [("rescal", "adagrad"), ("rescal+sp", "adagrad"),
-                                     ("rescal", "sgd")])
-def test_r_update_in_mtile_pass_is_bitwise_separate(built_lib, cuda_dev, dec, opt):
-    """VERDICT r5 item 4 (include/rae.h RAE_BILRUPD_MTILE): the second M-tile pass updates the
-    R (hybrid: C) block it staged, after its contractions, instead of the update launch's R
-    tiles -- the same gradient operands, K order and optimizer arithmetic, so parameters,
-    optimizer state and costs are BITWISE those of the separate update (C5 shape, bf16, two
-    epochs of three batches, graph-replayed).  auto picks the fused form here."""
-    from rae.data import synthetic_dataset
-    from rae.inducer import ReconstructInducer
-    m, r, s, l = 100, 200, 20, 100
-    out = {}
-    for form in ("mtile", "separate", "auto"):
-        data, gold = synthetic_dataset(3 * l, 2000, 10, seed=21)
-        ind = ReconstructInducer(data, gold, np.random.RandomState(2), 2, 0.1, l, r, m, s, 0.0,
-                                 0.0, opt, "rupd", dec, False, True, False, 1.0,
-                                 device=cuda_dev, graph_chunk=2, mfma_bf16=True,
-                                 kernel_forms={"bil_rupd": form})
-        ind.learn(verbose=False)
-        got = ind.engine.kernel_forms_in_use()["bil_rupd"]
-        assert got == (form if form != "auto" else "mtile"), (form, got)
-        acc = {}
-        if ind.optimizer.accumulator is not None:
-            acc = {f"acc_{k}": v.detach().cpu().numpy()
-                   for k, v in zip(ind.modelFunc.param_names, ind.optimizer.accumulator)}
-        out[form] = (_params(ind), acc, np.array(ind.epoch_costs))
-        ind._drop_engine()
-    for form in ("separate", "auto"):
-        assert np.array_equal(out[form][2], out["mtile"][2]), form
-        for k in out["mtile"][0]:
-            assert np.array_equal(out[form][0][k], out["mtile"][0][k]), (form, k)
-        for k in out["mtile"][1]:
-            assert np.array_equal(out[form][1][k], out["mtile"][1][k]), (form, k)
-
-
 def test_cursor_and_absolute_batch_launches_agree(built_lib, cuda_dev):
     # the two ways include/rae.h addresses a step's batch: a device cursor + offset
     # (rae_step_forward / rae_step_update) and the absolute index in the launch
