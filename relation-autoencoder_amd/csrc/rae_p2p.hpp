@@ -199,17 +199,25 @@ __device__ void p2p_pre(const StepArgs& a, int prologue, int nmb) {
     p2p_stores_done();
 }
 
-// update(b), pipelined form: owned row `row` of table tab was just written (its new values in
-// the lanes' vectors v[0..Q)): into the replica of every peer that reads it in batch b + 1
-template <class VT, int Q>
-__device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int row, const VT (&v)[Q],
-                                              int nv, int lane) {
-    if (!a.pipe) return;
+// update(b), pipelined form: the peers (bits) that read owned row `row` of table tab in batch
+// b + 1 -- loaded by the row task when it issues its parameter loads, so the byte's round trip
+// is not on the task's chain; 0 when not pipelined or b is the epoch's last batch
+__device__ __forceinline__ unsigned pipe_mark(const StepArgs& a, int tab, int row) {
+    if (!a.pipe) return 0u;
     const int64_t tb = step_batch(a) + 1;
-    if (tb >= epoch_batches(a)) return;
-    const unsigned mk = pipe_marks(a, tb, tab)[row / a.G] & ~(1u << a.rank);
+    if (tb >= epoch_batches(a)) return 0u;
+    // the row is wave-uniform: one word load the compiler can keep scalar (no VGPR held
+    // across the task)
+    const int q = __builtin_amdgcn_readfirstlane(row / a.G);
+    const uint32_t wd = reinterpret_cast<const uint32_t*>(pipe_marks(a, tb, tab))[q >> 2];
+    return __builtin_amdgcn_readfirstlane((wd >> (8 * (q & 3))) & 0xffu & ~(1u << a.rank));
+}
+// ... and once the row is written (its new values in the lanes' vectors v[0..Q)): into the
+// replica of every peer in mk
+template <class VT, int Q>
+__device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int row, unsigned mk,
+                                              const VT (&v)[Q], int nv, int lane) {
     if (!mk) return;
-    constexpr int VW = sizeof(VT) / sizeof(float);
     const int w = tab ? a.m : a.r;
     for (int p = 0; p < a.G; ++p) {
         if (!((mk >> p) & 1u)) continue;
@@ -220,14 +228,9 @@ __device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int ro
             if (c < nv) store_sys(d + c, v[q]);
         }
     }
-    (void)VW;
 }
-// ... and an entity row's Ab (lane 0)
-__device__ __forceinline__ void pipe_push_ab(const StepArgs& a, int row, float v) {
-    if (!a.pipe) return;
-    const int64_t tb = step_batch(a) + 1;
-    if (tb >= epoch_batches(a)) return;
-    const unsigned mk = pipe_marks(a, tb, 0)[row / a.G] & ~(1u << a.rank);
+// ... an entity row's Ab (one lane)
+__device__ __forceinline__ void pipe_push_ab(const StepArgs& a, int row, unsigned mk, float v) {
     for (int p = 0; p < a.G; ++p)
         if ((mk >> p) & 1u) store_sys(a.peers[p].Ab + row, v);
 }

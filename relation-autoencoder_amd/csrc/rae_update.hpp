@@ -407,14 +407,15 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
     }
 }
 
-// (pipelined peer-to-peer form: the new Ab also into the peers that read row e next batch)
+// (pipelined peer-to-peer form: the new Ab also into the peers mk that read row e next batch)
 template <int OPT>
-__device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, float aab0, float gb) {
+__device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, float aab0, float gb,
+                                          unsigned mk = 0u) {
     float ac = aab0;
     const float v = opt_update<OPT>(ab0, &ac, gb, a.lr);
     a.Ab[e] = v;
     if (OPT == 0) a.aAb[e] = ac;
-    pipe_push_ab(a, e, v);
+    if (mk) pipe_push_ab(a, e, mk, v);
 }
 
 template <int OPT, bool V4, int Q, int VS>
@@ -436,6 +437,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
 #endif
     const float ab0 = a.Ab[e];
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
+    const unsigned mk = pipe_mark(a, 0, e);
     g.zero();
     float gb = 0.f;
     if (seg.z - seg.y > RAE_VHEAVY) {
@@ -466,8 +468,8 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
         gb = wave_sum(gb);
     }
     apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
-    pipe_push_row(a, 0, e, pv.v, nv, lane);
-    if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb);
+    pipe_push_row(a, 0, e, mk, pv.v, nv, lane);
+    if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gb, mk);
 }
 
 // A very heavy row (> RAE_VHEAVY records) per workgroup: its sorted record list split into
@@ -487,11 +489,13 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
     float* arow = (OPT == 0) ? a.aA + (int64_t)e * r : nullptr;
     RowVec<V4, Q> pv, av, g;
     float ab0 = 0.f, aab0 = 0.f;
+    unsigned mk = 0u;
     if (w == 0 && !chunk) {
         pv.load(prow, nv, lane);
         if (OPT == 0) av.load(arow, nv, lane); else av.zero();
         ab0 = a.Ab[e];
         aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
+        mk = pipe_mark(a, 0, e);
     }
     g.zero();
     float gb = 0.f;
@@ -523,8 +527,8 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
             return;
         }
         apply_row<OPT, V4, Q>(prow, arow, pv, av, g, nv, a.lr, lane);
-        pipe_push_row(a, 0, e, pv.v, nv, lane);
-        if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gt);
+        pipe_push_row(a, 0, e, mk, pv.v, nv, lane);
+        if (lane == 0) ab_update<OPT>(a, e, ab0, aab0, gt, mk);
     }
 }
 
@@ -581,7 +585,8 @@ __device__ __forceinline__ void feature_accum(const StepArgs& a, int64_t ex0, in
 // W row f with gradient g: applied, or (lambda != 0) left in the dense scratch for k_dense_w
 template <int OPT, bool V4, int Q>
 __device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<V4, Q>& pv,
-                                               RowVec<V4, Q>& av, RowVec<V4, Q>& g, int lane) {
+                                               RowVec<V4, Q>& av, RowVec<V4, Q>& g, int lane,
+                                               unsigned mk = 0u) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
     const int m = a.m, nv = m / VW;
@@ -595,7 +600,7 @@ __device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<
     } else {
         float* arow = (OPT == 0 && a.aW) ? a.aW + (int64_t)f * m : nullptr;
         apply_row<OPT, V4, Q>(a.W + (int64_t)f * m, arow, pv, av, g, nv, a.lr, lane);
-        pipe_push_row(a, 1, f, pv.v, nv, lane);
+        pipe_push_row(a, 1, f, mk, pv.v, nv, lane);
     }
 }
 
@@ -610,6 +615,7 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
         pv.load(a.W + (int64_t)f * m, nv, lane);
         if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
     }
+    const unsigned mk = pipe_mark(a, 1, f);
 #ifdef RAE_STAMPS
     if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
         const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
@@ -637,7 +643,7 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
     } else {
         feature_accum<V4, Q>(a, ex0, base, seg.y, seg.z, seg.w, g, lane);
     }
-    feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
+    feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane, mk);
 }
 
 // a very heavy W row per workgroup (as wg_entity_row)
@@ -652,9 +658,11 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
     const int ch = (en - st + RAE_NWAVE - 1) / RAE_NWAVE;
     const int c0 = min(st + w * ch, en), c1 = min(c0 + ch, en);
     RowVec<V4, Q> pv, av, g;
+    unsigned mk = 0u;
     if (w == 0 && !a.reg_on && !chunk) {
         pv.load(a.W + (int64_t)f * m, nv, lane);
         if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
+        mk = pipe_mark(a, 1, f);
     }
     g.zero();
     if (c0 < c1) feature_accum<V4, Q>(a, ex0, base, c0, c1, seg.w, g, lane);
@@ -678,7 +686,7 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
             }
             return;
         }
-        feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane);
+        feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane, mk);
     }
 }
 
@@ -710,6 +718,7 @@ __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
         ab0 = a.Ab[row];
         aab0 = (OPT == 0) ? a.aAb[row] : 0.f;
     }
+    const unsigned mk = pipe_mark(a, isA ? 0 : 1, row);
     gs.zero();
     float gb = 0.f;
     const float* hp0 = a.hpart + (int64_t)f.y * a.hps;
@@ -738,10 +747,10 @@ __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
     }
     if (isA) {
         apply_row<OPT, V4, Q>(prow, arow, pv, av, gs, nv, a.lr, lane);
-        pipe_push_row(a, 0, row, pv.v, nv, lane);
-        if (lane == 0) ab_update<OPT>(a, row, ab0, aab0, gb);
+        pipe_push_row(a, 0, row, mk, pv.v, nv, lane);
+        if (lane == 0) ab_update<OPT>(a, row, ab0, aab0, gb, mk);
     } else {
-        feature_finish<OPT, V4, Q>(a, row, pv, av, gs, lane);
+        feature_finish<OPT, V4, Q>(a, row, pv, av, gs, lane, mk);
     }
 }
 

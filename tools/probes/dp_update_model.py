@@ -61,17 +61,21 @@ class NoPeers:
 
 def loopback_p2p_setup(eng):
     """Peers of a G-rank plan with no peer processes: every peer's exchange buffer / replica
-    is one local dummy buffer set, and peer p's signal words start (p - rank) words before this
-    rank's, so the push's add on "peer p's word (kind, rank)" lands on this rank's word
-    (kind, p) -- the count the wait for peer p expects."""
+    is a local dummy buffer set of its own (distinct addresses, as distinct GPUs would have:
+    pushes of one row to several peers are not stores to one address), and peer p's signal
+    words start (p - rank) words before this rank's, so the push's add on "peer p's word
+    (kind, rank)" lands on this rank's word (kind, p) -- the count the wait for peer p
+    expects."""
     import torch
     named = eng._named
-    eng._loop = [torch.zeros_like(eng.exchange_buf), torch.empty_like(named["W"]),
-                 torch.empty_like(named["A"]), torch.empty_like(named["Ab"])]
+    eng._loop = []
     sig = int(eng.lib.rae_p2p_signals(eng.plan))
     for p in range(eng.world_size):
         if p != eng.rank:
-            ex, W, A, Ab = (C.c_void_p(t.data_ptr()) for t in eng._loop)
+            bufs = [torch.zeros_like(eng.exchange_buf), torch.empty_like(named["W"]),
+                    torch.empty_like(named["A"]), torch.empty_like(named["Ab"])]
+            eng._loop.append(bufs)
+            ex, W, A, Ab = (C.c_void_p(t.data_ptr()) for t in bufs)
             rc = eng.lib.rae_set_peer(eng.plan, p, ex, W, A, Ab, C.c_void_p(sig + 4 * (p - eng.rank)))
             assert rc == 0, eng.lib.rae_last_error()
 
