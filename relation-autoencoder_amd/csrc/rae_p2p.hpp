@@ -217,6 +217,9 @@ __device__ __forceinline__ unsigned pipe_mark(const StepArgs& a, int tab, int ro
 template <class VT, int Q>
 __device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int row, unsigned mk,
                                               const VT (&v)[Q], int nv, int lane) {
+#if defined(RAE_DIAG) && defined(RAE_PIPE_NOPUSH)   // diagnostic A/B only: no update pushes
+    return;
+#endif
     if (!mk) return;
     const int w = tab ? a.m : a.r;
     for (int p = 0; p < a.G; ++p) {
@@ -225,7 +228,11 @@ __device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int ro
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int c = lane + RAE_WAVE * q;
+#if defined(RAE_DIAG) && defined(RAE_PIPE_PLAIN)   // diagnostic A/B only: plain stores
+            if (c < nv) d[c] = v[q];
+#else
             if (c < nv) store_sys(d + c, v[q]);
+#endif
         }
     }
 }
