@@ -440,11 +440,13 @@ template <int OPT, bool V4, int Q, bool WIRE>
 __global__ __launch_bounds__(RAE_BT) RAE_UPD_ATTR void k_update(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
     update_body<OPT, V4, Q, WIRE ? 2 : 0>(a, blockIdx.x, gridDim.x, lds);
+    if (a.pipe) p2p_stores_done();   // the row pushes acknowledged before the wave ends
 }
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) void k_update_bil(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
     update_body<OPT, V4, Q, 1>(a, blockIdx.x, gridDim.x, lds);
+    if (a.pipe) p2p_stores_done();
 }
 // The bilinear decoders' update phase in ONE launch: workgroups [0, gu) run k_update_bil's tasks
 // (Wb tiles, cost, A / W rows: latency-bound chains), the rest k_bil_rows' R tiles (16 rows
@@ -457,6 +459,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
     const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (wg < gu) {
         update_body<OPT, V4, Q, 1>(a, wg, gu, reinterpret_cast<float*>(smem));
+        if (a.pipe) p2p_stores_done();
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -474,6 +477,7 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
 template <int OPT, bool V4, int Q>
 __global__ __launch_bounds__(RAE_BT) void k_heavy_fin(StepArgs a) {
     heavy_fin<OPT, V4, Q>(a, blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6), threadIdx.x & 63);
+    if (a.pipe) p2p_stores_done();
 }
 
 // Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,

@@ -14,9 +14,8 @@
 //   k_p2p_recs   its l records into every peer's exchange buffer, at the same rows
 //   k_p2p_wait   (records): until every peer's records of batch b are here
 //   update(b)    the owned rows, as before
-// Signalling: after a push kernel a one-wave signal kernel fences at system scope and adds one
-// to the peer's signal word (kind, this rank) with a system-scope release -- a counter that
-// grows by one every step (fences per workgroup inside the pushes cost an L2 write-back each:
+// Signalling: after a push kernel a one-wave signal kernel adds one to the peer's signal word
+// (kind, this rank) with a system-scope atomic -- a counter that grows by one every step (fences per workgroup inside the pushes cost an L2 write-back each:
 // 55-81 us per step in the loopback model).  The waiting kernel (one wave: lane p watches peer
 // p) spins on relaxed system-scope loads until each counter reaches its expected value (kept in
 // this rank's private words, advanced by the wait kernel itself, so graph replays stay in
@@ -64,14 +63,16 @@ __device__ __forceinline__ void store_sys(float* p, float v) {
 }
 __device__ __forceinline__ void p2p_stores_done() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
 
-// k_p2p_signal (one wave, after a push kernel): the push's stores completed at system scope
-// before its waves ended (store_sys + vmcnt(0)); this fences at system scope once more and
-// counts one signal into every peer's (uncached) word (kind, rank)
+// k_p2p_signal (one wave, after a push kernel): every store of the pushes is a system-scope
+// write-through that its wave waited for (store_sys + vmcnt(0): the push kernels, and the
+// update kernels' row pushes of the pipelined form) -- complete at system scope before the
+// kernel boundary this launch follows -- so the add needs no release fence: a relaxed
+// system-scope add into every peer's (uncached) word (kind, rank).  (A release here would
+// write back this XCD's whole L2 -- the update's dirty parameter rows -- on every signal.)
 __device__ void p2p_signal(const StepArgs& a, int kind) {
-    __threadfence_system();
     if (threadIdx.x < a.G && threadIdx.x != a.rank) {
         unsigned* s = a.peers[threadIdx.x].sig + kind * a.G + a.rank;
-        __hip_atomic_fetch_add(s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
