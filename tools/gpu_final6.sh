@@ -65,6 +65,20 @@ print('$c', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: ro
         || { echo "stats $c failed"; tail -20 $O/stats_$c.err; exit 1; }
       cp $O/stats_$c/run_kernel_stats.csv $O/r06_${c}_kernel_stats.csv
       cut -c1-120 $O/stats_$c/run_kernel_stats.csv | head -10 ;;
+    drv)
+      # the driver's exact command (BENCH_rNN.json): 20 timed steps, 5 warm-up, CPU baseline
+      timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/r06_c3_bench_driver_cmd.json 2> $O/drv.err \
+        || { echo drv bench failed; tail -30 $O/drv.err; exit 1; }
+      python3 -c "
+import json; d=json.load(open('$O/r06_c3_bench_driver_cmd.json')); r=d['roofline']
+print('drv', round(d['value']), 'us/step', round(d['ms_per_step']*1e3, 2), {k: round(v, 2) for k, v in d['kernel_us'].items()}, 'frac', round(r['frac'], 4), 'traffic_current', r.get('traffic_current'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))" ;;
+    drvstats)
+      # rocprofv3 summary of the driver's exact command
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/drvstats -o run \
+        -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/drvstats.json 2> $O/drvstats.err) \
+        || { echo "drvstats failed"; tail -20 $O/drvstats.err; exit 1; }
+      cp $O/drvstats/run_kernel_stats.csv $O/r06_c3_driver_cmd_kernel_stats.csv
+      cut -c1-120 $O/drvstats/run_kernel_stats.csv | head -6 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
