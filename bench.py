@@ -273,8 +273,6 @@ def main():
                     help="--dp-xchg p2p with ranks on different GPUs (verified on ranks sharing "
                          "one GPU only; refused without this flag)")
     args = ap.parse_args()
-    if args.dp_update == "auto":
-        args.dp_update = CONFIGS[args.config].get("dp_update", "replicated")
     if args.dp_xchg != "collective":
         args.dp_update = "partitioned"
         args.kernel_form.append(f"dp_xchg={args.dp_xchg}")
@@ -285,6 +283,8 @@ def main():
     from rae.inducer import ReconstructInducer
 
     ws, rk, lrank = rdist.init()
+    if args.dp_update == "auto":         # one rank: the plan has no data-parallel update
+        args.dp_update = CONFIGS[args.config].get("dp_update", "replicated") if ws > 1 else "replicated"
     if ws != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
     # one GPU per local rank; ranks beyond the node's GPUs share them (a rehearsal of the
