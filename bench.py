@@ -48,9 +48,9 @@ CONFIGS = {
                name="C2 synthetic 100k triples K=30 embed=100 neg=10 sp"),
     "c3": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="sp", ntrue=100,
                name="C3 synthetic 1M triples K=100 embed=200 neg=20 sp (headline)"),
-    # dp_update: the data-parallel update form --dp-update auto picks (tools/probes/
-    # dp_update_model.py, DESIGN.md 4: at G = 8, l = 100 C4 projects 31.7 % partitioned vs
-    # 27.2 % replicated over RCCL, C3 24.5 % vs 26.3 %)
+    # dp_update: the data-parallel update form --dp-update auto picks at N > 1 (tools/probes/
+    # dp_update_model.py, DESIGN.md 4: at G = 8, l = 100 C4 projects 32.6 % partitioned vs
+    # 27.5 % replicated over RCCL, C3 24.0 % vs 25.4 %)
     "c4": dict(N=10_000_000, d=2 ** 20, m=300, r=300, s=50, dec="sp", ntrue=300,
                dp_update="partitioned", name="C4 synthetic 10M triples K=300 embed=300 neg=50 sp"),
     "c5": dict(N=1_000_000, d=2 ** 17, m=100, r=200, s=20, dec="rescal", ntrue=100, bf16=True,
