@@ -303,7 +303,7 @@ __host__ __device__ constexpr int update_lds_floats() {
 // (the fused bilinear kernel puts the update's workgroups in front of the R-tile ones)
 // VS: where the A-row tasks find the record vectors (rae_update.hpp entity_accum): 0 SP records
 // (single rank), 1 bilinear records, 2 the SP wire record's vector buffer (data parallel)
-template <int OPT, bool V4, int Q, int VS>
+template <int OPT, bool V4, int Q, int VS, bool PP = false>
 __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngrid, float* lds) {
     typedef typename VecT<V4>::T VT;
     constexpr int kF = update_lds_floats<V4, Q>() - RAE_NWAVE;
@@ -401,10 +401,10 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         const bool isA = seg.x >= 0;
         RAE_FIRST(isA ? 8 : 9);
         if (isA) {
-            wg_entity_row<OPT, V4, Q, VS>(a, slot, seg, w, lane, spart, sgb);
+            wg_entity_row<OPT, V4, Q, VS, PP>(a, slot, seg, w, lane, spart, sgb);
         } else {
             seg.x = ~seg.x;
-            wg_feature_row<OPT, V4, Q>(a, ex0, slot, seg, w, lane, spart);
+            wg_feature_row<OPT, V4, Q, PP>(a, ex0, slot, seg, w, lane, spart);
         }
         RAE_WAVE_END();
         return;
@@ -423,8 +423,8 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
         const bool curA = cur.x >= 0;
         if (!curA) cur.x = ~cur.x;
         RAE_FIRST((curA ? 4 : 5) + (cur.z - cur.y > RAE_HEAVY ? 2 : 0));
-        if (curA) task_entity_row<OPT, V4, Q, VS>(a, slot, cur, lane);
-        else task_feature_row<OPT, V4, Q>(a, ex0, slot, cur, lane);
+        if (curA) task_entity_row<OPT, V4, Q, VS, PP>(a, slot, cur, lane);
+        else task_feature_row<OPT, V4, Q, PP>(a, ex0, slot, cur, lane);
         RAE_WAVE_END();
     }
 #undef RAE_FIRST
@@ -439,27 +439,27 @@ __device__ __forceinline__ void update_body(const StepArgs& a, int wg0, int ngri
 template <int OPT, bool V4, int Q, bool WIRE>
 __global__ __launch_bounds__(RAE_BT) RAE_UPD_ATTR void k_update(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
-    update_body<OPT, V4, Q, WIRE ? 2 : 0>(a, blockIdx.x, gridDim.x, lds);
-    if (a.pipe) p2p_stores_done();   // the row pushes acknowledged before the wave ends
+    update_body<OPT, V4, Q, WIRE ? 2 : 0, WIRE>(a, blockIdx.x, gridDim.x, lds);
+    if (WIRE && a.pipe) p2p_stores_done();   // the row pushes acknowledged before the wave ends
 }
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __global__ __launch_bounds__(RAE_BT) void k_update_bil(StepArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[update_lds_floats<V4, Q>()];
-    update_body<OPT, V4, Q, 1>(a, blockIdx.x, gridDim.x, lds);
-    if (a.pipe) p2p_stores_done();
+    update_body<OPT, V4, Q, 1, PP>(a, blockIdx.x, gridDim.x, lds);
+    if (PP && a.pipe) p2p_stores_done();
 }
 // The bilinear decoders' update phase in ONE launch: workgroups [0, gu) run k_update_bil's tasks
 // (Wb tiles, cost, A / W rows: latency-bound chains), the rest k_bil_rows' R tiles (16 rows
 // (i, j) x all m per wave: the HBM-heavy R sweep) -- the two have no data in common, so the
 // row chains run under the R sweep instead of after it.  Dynamic LDS: the R tiles' (DMA'd R and
 // accumulator rows); an update workgroup carves its partials from the same allocation.
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x);
     if (wg < gu) {
-        update_body<OPT, V4, Q, 1>(a, wg, gu, reinterpret_cast<float*>(smem));
-        if (a.pipe) p2p_stores_done();
+        update_body<OPT, V4, Q, 1, PP>(a, wg, gu, reinterpret_cast<float*>(smem));
+        if (PP && a.pipe) p2p_stores_done();
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -474,10 +474,10 @@ __global__ __launch_bounds__(RAE_BT) void k_bil_update(StepArgs a, int gu) {
 #endif
 
 // rows split into chunks (StepArgs::hch): each row's chunk sums combined in order + its update
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __global__ __launch_bounds__(RAE_BT) void k_heavy_fin(StepArgs a) {
-    heavy_fin<OPT, V4, Q>(a, blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6), threadIdx.x & 63);
-    if (a.pipe) p2p_stores_done();
+    heavy_fin<OPT, V4, Q, PP>(a, blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6), threadIdx.x & 63);
+    if (PP && a.pipe) p2p_stores_done();
 }
 
 // Dense W sweep (lambda1/lambda2 != 0): g = sparse-part scratch + l1adj*sgn(W) + 2*l2adj*W,
@@ -1319,14 +1319,24 @@ static void launch_update_b(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
         constexpr size_t lu = 4 * update_lds_floats<V4, 2>();
         if (RAE_BIL_FUSED_UPD && lr >= lu) {
             const dim3 gf(gu.x + gr.x);
-            if (p->q == 1) RAE_LAUNCH(p, (k_bil_update<OPT, V4, 1>), gf, bt, lr, st, a, (int)gu.x);
-            else RAE_LAUNCH(p, (k_bil_update<OPT, V4, 2>), gf, bt, lr, st, a, (int)gu.x);
+            if (a.pipe) {     // (the pipelined peer-to-peer form's row pushes compiled in)
+                if (p->q == 1) RAE_LAUNCH(p, (k_bil_update<OPT, V4, 1, true>), gf, bt, lr, st, a, (int)gu.x);
+                else RAE_LAUNCH(p, (k_bil_update<OPT, V4, 2, true>), gf, bt, lr, st, a, (int)gu.x);
+            } else {
+                if (p->q == 1) RAE_LAUNCH(p, (k_bil_update<OPT, V4, 1>), gf, bt, lr, st, a, (int)gu.x);
+                else RAE_LAUNCH(p, (k_bil_update<OPT, V4, 2>), gf, bt, lr, st, a, (int)gu.x);
+            }
             return;
         }
         if (lr) RAE_LAUNCH(p, (k_bil_rows<OPT, true>), gr, bt, lr, st, a);
         else RAE_LAUNCH(p, (k_bil_rows<OPT, false>), gr, bt, 0, st, a);
-        if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
-        else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
+        if (a.pipe) {
+            if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1, true>), gu, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2, true>), gu, bt, 0, st, a);
+        } else {
+            if (p->q == 1) RAE_LAUNCH(p, (k_update_bil<OPT, V4, 1>), gu, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_update_bil<OPT, V4, 2>), gu, bt, 0, st, a);
+        }
     } else {
         // the data-parallel SP update (wire records: vectors in the vector buffer, dense
         // partials) and the single-rank one are separate instantiations
@@ -1350,6 +1360,28 @@ static void launch_update_q(rae_plan* p, dim3 gu, dim3 bt, hipStream_t st, const
     else launch_update_v<OPT, false>(p, gu, bt, st, a);
 }
 
+// k_heavy_fin for the plan's optimizer / vector width / row slots (PP: pipelined pushes)
+template <bool PP>
+static void launch_heavy_fin(rae_plan* p, dim3 gh, dim3 bt, hipStream_t st, const StepArgs& a) {
+    if (a.opt == RAE_OPT_ADAGRAD) {
+        if (p->v4) {
+            if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, true, 1, PP>), gh, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_heavy_fin<0, true, 2, PP>), gh, bt, 0, st, a);
+        } else {
+            if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, false, 1, PP>), gh, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_heavy_fin<0, false, 2, PP>), gh, bt, 0, st, a);
+        }
+    } else {
+        if (p->v4) {
+            if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, true, 1, PP>), gh, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_heavy_fin<1, true, 2, PP>), gh, bt, 0, st, a);
+        } else {
+            if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, false, 1, PP>), gh, bt, 0, st, a);
+            else RAE_LAUNCH(p, (k_heavy_fin<1, false, 2, PP>), gh, bt, 0, st, a);
+        }
+    }
+}
+
 static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStream_t st) {
     StepArgs a = p->args;
     a.cursor = cursor;
@@ -1369,23 +1401,8 @@ static int launch_update(rae_plan* p, const int64_t* cursor, int64_t off, hipStr
     HIPCHK(hipGetLastError());
     if (a.hch) {              // the rows split into chunks: their chunk sums combined + updated
         const dim3 gh(ceil_div(a.HF, RAE_NWAVE));
-        if (a.opt == RAE_OPT_ADAGRAD) {
-            if (p->v4) {
-                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, true, 1>), gh, bt, 0, st, a);
-                else RAE_LAUNCH(p, (k_heavy_fin<0, true, 2>), gh, bt, 0, st, a);
-            } else {
-                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<0, false, 1>), gh, bt, 0, st, a);
-                else RAE_LAUNCH(p, (k_heavy_fin<0, false, 2>), gh, bt, 0, st, a);
-            }
-        } else {
-            if (p->v4) {
-                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, true, 1>), gh, bt, 0, st, a);
-                else RAE_LAUNCH(p, (k_heavy_fin<1, true, 2>), gh, bt, 0, st, a);
-            } else {
-                if (p->q == 1) RAE_LAUNCH(p, (k_heavy_fin<1, false, 1>), gh, bt, 0, st, a);
-                else RAE_LAUNCH(p, (k_heavy_fin<1, false, 2>), gh, bt, 0, st, a);
-            }
-        }
+        if (a.pipe) launch_heavy_fin<true>(p, gh, bt, st, a);
+        else launch_heavy_fin<false>(p, gh, bt, st, a);
         HIPCHK(hipGetLastError());
     }
     if (a.reg_on) {

@@ -203,10 +203,11 @@ __device__ void p2p_pre(const StepArgs& a, int prologue, int nmb) {
 // update(b), pipelined form: the peers (bits) that read owned row `row` of table tab in batch
 // b + 1 -- loaded by the row task when it issues its parameter loads, so the byte's round trip
 // is not on the task's chain; 0 when not pipelined or b is the epoch's last batch
+// PP: the update instantiation may run a pipelined plan (data parallel); the single-rank
+// instantiations compile the pushes out (a runtime-off branch still cost the C4 update 1.3 us)
+template <bool PP>
 __device__ __forceinline__ unsigned pipe_mark(const StepArgs& a, int tab, int row) {
-#if defined(RAE_DIAG) && defined(RAE_PIPE_OFF)     // diagnostic A/B only: the pushes compiled out
-    return 0u;
-#endif
+    if constexpr (!PP) return 0u;
     if (!a.pipe) return 0u;
     const int64_t tb = step_batch(a) + 1;
     if (tb >= epoch_batches(a)) return 0u;

@@ -418,7 +418,7 @@ __device__ __forceinline__ void ab_update(const StepArgs& a, int e, float ab0, f
     if (mk) pipe_push_ab(a, e, mk, v);
 }
 
-template <int OPT, bool V4, int Q, int VS>
+template <int OPT, bool V4, int Q, int VS, bool PP = false>
 __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     const int r = a.r, nv = r / VW;
@@ -437,7 +437,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
 #endif
     const float ab0 = a.Ab[e];
     const float aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
-    const unsigned mk = pipe_mark(a, 0, e);
+    const unsigned mk = pipe_mark<PP>(a, 0, e);
     g.zero();
     float gb = 0.f;
     if (seg.z - seg.y > RAE_VHEAVY) {
@@ -475,7 +475,7 @@ __device__ void task_entity_row(const StepArgs& a, int64_t slot, int4 seg, int l
 // A very heavy row (> RAE_VHEAVY records) per workgroup: its sorted record list split into
 // four contiguous chunks, one per wave; wave 0 sums the partial rows in wave order and applies
 // the update (its parameter loads in flight meanwhile).  spart: RAE_NWAVE * 64 * Q vectors.
-template <int OPT, bool V4, int Q, int VS>
+template <int OPT, bool V4, int Q, int VS, bool PP = false>
 __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, int lane,
                               typename VecT<V4>::T* spart, float* sgb) {
     constexpr int VW = V4 ? 4 : 1;
@@ -495,7 +495,7 @@ __device__ void wg_entity_row(const StepArgs& a, int64_t slot, int4 seg, int w, 
         if (OPT == 0) av.load(arow, nv, lane); else av.zero();
         ab0 = a.Ab[e];
         aab0 = (OPT == 0) ? a.aAb[e] : 0.f;
-        mk = pipe_mark(a, 0, e);
+        mk = pipe_mark<PP>(a, 0, e);
     }
     g.zero();
     float gb = 0.f;
@@ -583,7 +583,7 @@ __device__ __forceinline__ void feature_accum(const StepArgs& a, int64_t ex0, in
 }
 
 // W row f with gradient g: applied, or (lambda != 0) left in the dense scratch for k_dense_w
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<V4, Q>& pv,
                                                RowVec<V4, Q>& av, RowVec<V4, Q>& g, int lane,
                                                unsigned mk = 0u) {
@@ -604,7 +604,7 @@ __device__ __forceinline__ void feature_finish(const StepArgs& a, int f, RowVec<
     }
 }
 
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int4 seg, int lane) {
     constexpr int VW = V4 ? 4 : 1;
     const int m = a.m, nv = m / VW;
@@ -615,7 +615,7 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
         pv.load(a.W + (int64_t)f * m, nv, lane);
         if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
     }
-    const unsigned mk = pipe_mark(a, 1, f);
+    const unsigned mk = pipe_mark<PP>(a, 1, f);
 #ifdef RAE_STAMPS
     if (a.stamps && lane == 0) {   // diagnostic: the row's segment has arrived (prow issued)
         const int gw_ = __builtin_amdgcn_readfirstlane(blockIdx.x * RAE_NWAVE + (threadIdx.x >> 6));
@@ -643,11 +643,11 @@ __device__ void task_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, i
     } else {
         feature_accum<V4, Q>(a, ex0, base, seg.y, seg.z, seg.w, g, lane);
     }
-    feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane, mk);
+    feature_finish<OPT, V4, Q, PP>(a, f, pv, av, g, lane, mk);
 }
 
 // a very heavy W row per workgroup (as wg_entity_row)
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int4 seg, int w,
                                int lane, typename VecT<V4>::T* spart) {
     constexpr int VW = V4 ? 4 : 1;
@@ -662,7 +662,7 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
     if (w == 0 && !a.reg_on && !chunk) {
         pv.load(a.W + (int64_t)f * m, nv, lane);
         if (OPT == 0) av.load(a.aW + (int64_t)f * m, nv, lane); else av.zero();
-        mk = pipe_mark(a, 1, f);
+        mk = pipe_mark<PP>(a, 1, f);
     }
     g.zero();
     if (c0 < c1) feature_accum<V4, Q>(a, ex0, base, c0, c1, seg.w, g, lane);
@@ -686,14 +686,14 @@ __device__ void wg_feature_row(const StepArgs& a, int64_t ex0, int64_t slot, int
             }
             return;
         }
-        feature_finish<OPT, V4, Q>(a, f, pv, av, g, lane, mk);
+        feature_finish<OPT, V4, Q, PP>(a, f, pv, av, g, lane, mk);
     }
 }
 
 // k_heavy_fin: entry e of the slot's combine list -- a row split into chunks: the chunks'
 // partial sums in chunk order (chunk k = records [st + k hch, ...) of the row's sorted list),
 // then the update, as the unsplit row task would apply it (one wave per row)
-template <int OPT, bool V4, int Q>
+template <int OPT, bool V4, int Q, bool PP = false>
 __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
     typedef typename VecT<V4>::T VT;
     constexpr int VW = V4 ? 4 : 1;
@@ -718,7 +718,7 @@ __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
         ab0 = a.Ab[row];
         aab0 = (OPT == 0) ? a.aAb[row] : 0.f;
     }
-    const unsigned mk = pipe_mark(a, isA ? 0 : 1, row);
+    const unsigned mk = pipe_mark<PP>(a, isA ? 0 : 1, row);
     gs.zero();
     float gb = 0.f;
     const float* hp0 = a.hpart + (int64_t)f.y * a.hps;
@@ -750,7 +750,7 @@ __device__ void heavy_fin(const StepArgs& a, int e, int lane) {
         pipe_push_row(a, 0, row, mk, pv.v, nv, lane);
         if (lane == 0) ab_update<OPT>(a, row, ab0, aab0, gb, mk);
     } else {
-        feature_finish<OPT, V4, Q>(a, row, pv, av, gs, lane, mk);
+        feature_finish<OPT, V4, Q, PP>(a, row, pv, av, gs, lane, mk);
     }
 }
 
