@@ -51,7 +51,7 @@ __global__ __launch_bounds__(RAE_FBT) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void k_forward(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t g = step_batch(a);
-    if constexpr (D::fixed && V4) sp_example_fast<D>(a, g, blockIdx.x, smem);
+    if constexpr (FastSP<D>::ok) sp_example_fast<D>(a, g, blockIdx.x, smem);
     else sp_example<V4, D>(a, g, blockIdx.x, smem);
 }
 

@@ -201,6 +201,16 @@ __device__ __forceinline__ void vfma(float& acc, float s, float v) { acc += s * 
 __device__ __forceinline__ void vfma(float4& acc, float s, float4 v) {
     acc.x += s * v.x; acc.y += s * v.y; acc.z += s * v.z; acc.w += s * v.w;
 }
+// vectors of VW floats (1, 2, 4): the fast forward's m-vectors go two wide when m is even but
+// not a multiple of 4 (C2: m = 30)
+template <int VW> struct VecW { typedef float T; };
+template <> struct VecW<2> { typedef float2 T; };
+template <> struct VecW<4> { typedef float4 T; };
+__device__ __forceinline__ float vdot(float2 a, float2 b) { return a.x * b.x + a.y * b.y; }
+__device__ __forceinline__ void vzero(float2& a) { a = make_float2(0.f, 0.f); }
+__device__ __forceinline__ void vfma(float2& acc, float s, float2 v) {
+    acc.x += s * v.x; acc.y += s * v.y;
+}
 // Exchange-record loads through one buffer resource: the record's offset rides in the scalar
 // soffset, the lane's column in a 32-bit voffset -- one SGPR per load instead of a 64-bit
 // address pair, which is what lets the update's wide rounds fit its VGPR budget (RAE_UPD_WPE).

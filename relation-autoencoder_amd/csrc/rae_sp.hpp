@@ -193,10 +193,10 @@ __device__ __forceinline__ void gather_rows_dma(const StepArgs& a, const D& Dm, 
 // group gid (16 lanes) owns rows i = gid + NG*ra, lane q owns column vectors c = q + 16*cc.
 // Fixed shapes that fit keep the whole pair resident for both matvecs; otherwise the
 // matrices stream through the same registers chunk by chunk.
-template <bool V4, class D>
-struct CCache {
-    typedef typename VecT<V4>::T VT;
-    static constexpr int VW = V4 ? 4 : 1;
+template <int VW_, class D>
+struct CCacheW {
+    typedef typename VecW<VW_>::T VT;
+    static constexpr int VW = VW_;
     static constexpr int RA0 = D::fixed ? (DimT<D>::r + RAE_NG - 1) / RAE_NG : 7;
     static constexpr int CC0 = D::fixed ? (DimT<D>::m / VW + 15) / 16 : 2;
     static constexpr bool FITS = D::fixed && RA0 <= 7 && CC0 <= 2;
@@ -227,6 +227,7 @@ struct CCache {
         }
     }
 };
+template <bool V4, class D> using CCache = CCacheW<V4 ? 4 : 1, D>;
 
 // wC1 = C1.P, wC2 = C2.P  -> S.swC1, S.swC2
 template <bool V4, class D>
@@ -981,11 +982,22 @@ __device__ __forceinline__ void fast_softmax(const StepArgs& a, ExampleSmem& S, 
 // decoder matrices are needed (lds_barrier), so the ~200 KB of bulk loads per CU overlap
 // the chain instead of sitting in front of it.  Softmax and the score coefficients use
 // hardware exp/log/rcp; the coefficient work is spread over 2s lanes.
+template <class D> struct FastSP { static constexpr int VM = 4; static constexpr bool ok = false; };
+template <int M, int R, int S> struct FastSP<FixDims<M, R, S>> {
+    // the m-vectors (W rows, C1 / C2 columns, P) four wide, or two wide for an even m that is
+    // not a multiple of 4 (C2: m = 30, 120-B rows at 8-B alignment)
+    static constexpr int VM = M % 4 == 0 ? 4 : 2;
+    static constexpr bool ok = M % 2 == 0 && R % 4 == 0 && S <= 32 && M / VM <= 32 &&
+                               R / 4 <= RAE_WAVE;
+};
 template <class D>
 __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem) {
-    static_assert(D::fixed && D::m % 4 == 0 && D::r % 4 == 0 && D::s <= 32, "fast SP path");
+    static_assert(FastSP<D>::ok, "fast SP path");
     constexpr int m = D::m, r = D::r, s = D::s, NR = 1 + 2 * s, NJ = 2 + 2 * s;
-    constexpr int MV = m / 4, NSL = 256 / MV, KF = 3;
+    constexpr int VM = FastSP<D>::VM;
+    typedef typename VecW<VM>::T MT;
+    typedef CCacheW<VM, D> CCF;
+    constexpr int MV = m / VM, NSL = 256 / MV, KF = 3;
     constexpr int r4 = r, mp = ((m + 255) / 256) * 256;
     const D Dm(a);
     // wave index as a scalar: role branches are then uniform control flow (s_cbranch on an
@@ -1002,7 +1014,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
 #ifdef RAE_STAMPS
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
 #endif
-    CCache<true, D> cc_;
+    CCF cc_;
 #if RAE_FWD_CWAIT && RAE_FWD_CEARLY47
     // waves 4-7 have no load on the chain: their half of C goes out at once (the other half
     // follows the W rows of waves 0-3), so C's ingest starts ~1 us earlier
@@ -1047,7 +1059,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     if (nf > a.dcap) {                       // longer than the descriptor holds: general path
 #endif
         lds_barrier();
-        sp_example<true, D>(a, g, bl, smem);
+        sp_example<VM == 4, D>(a, g, bl, smem);
         return;
     }
     if (a.values) {                          // non-binary features: their values
@@ -1060,9 +1072,9 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     // queue are in issue order, so the 5 KB of W rows the chain waits on go out first, the
     // A rows (needed after C.P) next, and the 160 KB of decoder matrices last.
     // W rows (waves 0-3): slot = feature lane group, c = float4 column.
-    const float4* W4 = reinterpret_cast<const float4*>(a.W);
+    const MT* Wm = reinterpret_cast<const MT*>(a.W);
     const int slot = tid / MV, c = tid - slot * MV;
-    float4 wv[KF];
+    MT wv[KF];
     float fv[KF];
     if (w < 4) {
 #pragma unroll
@@ -1070,7 +1082,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
             const int f = slot + NSL * k;
             const bool ok = slot < NSL && f < nf;
             const int fi = RAE_KO_W ? 0 : S.sfidx[f < 256 ? f : 255];   // knockout: row 0
-            wv[k] = W4[(int64_t)(ok ? fi : 0) * MV + c];
+            wv[k] = Wm[(int64_t)(ok ? fi : 0) * MV + c];
             fv[k] = ok ? S.sfval[f < 256 ? f : 255] : 0.f;
         }
     }
@@ -1104,11 +1116,11 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     asm volatile("" ::: "memory");
     if (!RAE_FWD_CEARLY47 || w < 4) cc_.load(a, Dm, 0, 0);
     if (w < 4) {
-        float4 acc;
+        MT acc;
         vzero(acc);
 #pragma unroll
         for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
-        if (slot < NSL) reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
+        if (slot < NSL) reinterpret_cast<MT*>(S.spart)[slot * MV + c] = acc;
     }
     if (false) {
 #else
@@ -1116,16 +1128,16 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
 #endif
         asm volatile("" ::: "memory");
         cc_.load(a, Dm, 0, 0);
-        float4 acc;
+        MT acc;
         vzero(acc);
 #pragma unroll
         for (int k = 0; k < KF; ++k) vfma(acc, fv[k], wv[k]);
         if (slot < NSL) {
 #if !RAE_FWD_CWAIT
             for (int f = slot + NSL * KF; f < nf; f += NSL)      // rows with > NSL*KF features
-                vfma(acc, S.sfval[f], W4[(int64_t)S.sfidx[f] * MV + c]);
+                vfma(acc, S.sfval[f], Wm[(int64_t)S.sfidx[f] * MV + c]);
 #endif
-            reinterpret_cast<float4*>(S.spart)[slot * MV + c] = acc;
+            reinterpret_cast<MT*>(S.spart)[slot * MV + c] = acc;
         }
     } else if (!RAE_FWD_CWAIT) {
         gather_rows_dma<true>(a, Dm, S, NR, 1, 4, 4);
@@ -1169,18 +1181,23 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
         // wC1 = C1.P, wC2 = C2.P: the 2*RA partial dots in C's load order (each waits for its
         // own loads only), then the 2*RA group reductions as independent interleaved DPP
         // chains, then one masked store block
-        typedef CCache<true, D> CC_;
-        static_assert(CC_::FITS && CC_::CC == 2, "fast path keeps C1/C2 in registers");
+        typedef CCF CC_;
+        static_assert(CC_::FITS && CC_::CC <= 2, "fast path keeps C1/C2 in registers");
         const int gid = tid >> 4, q = tid & 15;
-        const float4* Pv = reinterpret_cast<const float4*>(S.sP);
-        const float4 pa = Pv[q], pb = Pv[q + 16];              // zero beyond m (padded)
+        const MT* Pv = reinterpret_cast<const MT*>(S.sP);
+        MT pv[CC_::CC];
+#pragma unroll
+        for (int cc = 0; cc < CC_::CC; ++cc) pv[cc] = Pv[q + 16 * cc];   // zero beyond m (padded)
         float s1[CC_::RA], s2[CC_::RA];
 #pragma unroll
         for (int ra = 0; ra < CC_::RA; ++ra) {
-            s1[ra] = vdot(cc_.c1[ra][0], pa);
-            s2[ra] = vdot(cc_.c2[ra][0], pa);
-            s1[ra] += vdot(cc_.c1[ra][1], pb);
-            s2[ra] += vdot(cc_.c2[ra][1], pb);
+            s1[ra] = vdot(cc_.c1[ra][0], pv[0]);
+            s2[ra] = vdot(cc_.c2[ra][0], pv[0]);
+#pragma unroll
+            for (int cc = 1; cc < CC_::CC; ++cc) {
+                s1[ra] += vdot(cc_.c1[ra][cc], pv[cc]);
+                s2[ra] += vdot(cc_.c2[ra][cc], pv[cc]);
+            }
         }
 #pragma unroll
         for (int ra = 0; ra < CC_::RA; ++ra) {
@@ -1340,11 +1357,11 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
     // dP = C1^T dw1 + C2^T dw2: per-wave partials (rows held in registers), reduced over the
     // wave's 4 lane groups; the 8 wave partials are summed by wave 0 below
     {
-        typedef CCache<true, D> CC_;
+        typedef CCF CC_;
         const int gid = tid >> 4, q = tid & 15;
-        float4 acc[CC_::CC];
+        MT acc[CC_::CC];
 #pragma unroll
-        for (int cc = 0; cc < CC_::CC; ++cc) acc[cc] = z4;
+        for (int cc = 0; cc < CC_::CC; ++cc) vzero(acc[cc]);
         float d1[CC_::RA], d2[CC_::RA];              // branch-free: all LDS reads issue at once
 #pragma unroll
         for (int ra = 0; ra < CC_::RA; ++ra) {
@@ -1362,7 +1379,7 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
                 vfma(acc[cc], e2, cc_.c2[ra][cc]);
             }
         }
-        if constexpr (CC_::CC == 2) {
+        if constexpr (VM == 4 && CC_::CC == 2) {
             // transpose-reduce the 8 partials over the wave's 4 lane groups with permlane
             // swaps: each swap + add halves two values at once (6 swaps instead of 16), and
             // leaves lane group G holding value {0,2,1,3}[G] of each float4
@@ -1395,12 +1412,12 @@ __device__ void sp_example_fast(const StepArgs& a, int64_t g, int bl, char* smem
             for (int cc = 0; cc < CC_::CC; ++cc) {
                 float* v = reinterpret_cast<float*>(&acc[cc]);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < VM; ++e) {
                     v[e] += __uint_as_float(xor16_u32(__float_as_uint(v[e])));
                     v[e] += __uint_as_float(xor32_u32(__float_as_uint(v[e])));
                 }
                 const int col = q + 16 * cc;
-                if (lane < 16 && col < MV) reinterpret_cast<float4*>(S.spart + w * mp)[col] = acc[cc];
+                if (lane < 16 && col < MV) reinterpret_cast<MT*>(S.spart + w * mp)[col] = acc[cc];
             }
         }
     }
