@@ -368,29 +368,32 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
         const int b = rec / NJ, j = rec - b * NJ;
         const int rb = b * a.lay.rec;
         const float* er = a.ex + rb + a.lay.ocoef + 2 * j;
-        float cj = er[0];
+        const float cj = er[0];
         const float ga = er[1];
-        if (lane >= n) cj = 0.f;
-        gb += lane < n ? ga : 0.f;
         const int vo = (EXT ? b * a.vbs : rb) + (j == 0 ? oG1 : (j == 1 ? vo1 : (j < 2 + s ? oV1 : oV2)));
         // one round: U record vectors loaded (all issued before the first FMA), then summed
-        // in record order -- the same order for every U, so the round width is free
+        // in record order -- the same order for every U, so the round width is free.  The
+        // vectors' offsets need only the record ids: their loads are issued before the first
+        // use of the coefficients (c_j, gamma_j), whose round trip then overlaps theirs instead
+        // of preceding them (the compiler waits at a value's first use)
         auto round = [&](auto Uc, int k0) {
             constexpr int U = decltype(Uc)::value;
             VT v[U][Q];
             float ck[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                const int src = min(k0 + k, n - 1);
-                const int ok = __builtin_amdgcn_readlane(vo, src);
-                ck[k] = (k0 + k < n) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj), src))
-                                     : 0.f;
+                const int ok = __builtin_amdgcn_readlane(vo, min(k0 + k, n - 1));
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int c = lane + RAE_WAVE * q;
                     rb_.load(v[k][q], (c < nv ? c : 0) * VW, ok);
                 }
             }
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                ck[k] = (k0 + k < n)
+                    ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj), min(k0 + k, n - 1)))
+                    : 0.f;
 #pragma unroll
             for (int k = 0; k < U; ++k)
 #pragma unroll
@@ -404,6 +407,7 @@ __device__ __forceinline__ void entity_accum(const StepArgs& a, int64_t base, in
 #pragma clang loop unroll(disable)
             for (int k0 = 0; k0 < n; k0 += UNRH) round(IntC<UNRH>{}, k0);
         }
+        gb += lane < n ? ga : 0.f;
     }
 }
 
