@@ -52,14 +52,25 @@ namespace rae {
 #define RAE_P2P_TIMEOUT_DEFAULT 500000000ull   // s_memrealtime ticks (100 MHz): 5 s
 
 // system-scope write-through stores into a peer's memory (sc0 sc1: not held in this GPU's L2);
-// the caller's wave waits for them with p2p_stores_done() before it ends
-__device__ __forceinline__ void store_sys(float4* p, float4 v) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(w) : "memory");
+// the caller's wave waits for them with p2p_stores_done() before it ends.  Buffer-store
+// builtins (cache-policy operand 17 = sc0 sc1) rather than inline asm: the compiler's hazard
+// and wait-count passes see these stores (an inline-asm store they cannot see lets them reuse
+// or wait wrongly around it -- measured: asm sc1 row stores in the update gave non-finite
+// costs, the same stores as builtins did not; profiles/r06_ab.txt).
+// base: a wave-uniform base pointer (made scalar here); c: the lane's element index.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const float* base) {
+    const uint64_t u = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    float* b = reinterpret_cast<float*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, -1, 0x00020000);
 }
-__device__ __forceinline__ void store_sys(float* p, float v) {
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+__device__ __forceinline__ void store_sys(const float* base, int c, float4 v) {
+    const rae_v4u u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(u, sys_rsrc(base), c * 16, 0, 17);
+}
+__device__ __forceinline__ void store_sys(const float* base, int c, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), sys_rsrc(base), c * 4, 0, 17);
 }
 __device__ __forceinline__ void p2p_stores_done() { asm volatile("s_waitcnt vmcnt(0)" : : : "memory"); }
 
@@ -86,11 +97,11 @@ __device__ void p2p_push_records(const StepArgs& a) {
     if (a.pipe && (int64_t)blockIdx.x >= nrb) {
         const int64_t b = step_batch(a);
         // (stored like the pushes, so every store of this kernel is one kind)
-        float4* pm = reinterpret_cast<float4*>(a.pm + (int64_t)((b + 1) & 1) * (a.pmA + a.pmW));
+        const float* pm = reinterpret_cast<const float*>(a.pm + (int64_t)((b + 1) & 1) * (a.pmA + a.pmW));
         const int64_t nw4 = (a.pmA + a.pmW) / 4;                      // pmA, pmW multiples of 4
         for (int64_t i = (blockIdx.x - nrb) * blockDim.x + threadIdx.x; i < nw4;
              i += (gridDim.x - nrb) * blockDim.x)
-            store_sys(pm + i, make_float4(0.f, 0.f, 0.f, 0.f));
+            store_sys(pm, (int)i, make_float4(0.f, 0.f, 0.f, 0.f));
         p2p_stores_done();
         return;
     }
@@ -99,7 +110,7 @@ __device__ void p2p_push_records(const StepArgs& a) {
     if (i >= n4) return;
     const float4 v = reinterpret_cast<const float4*>(a.ex)[o4 + i];
     for (int p = 0; p < a.G; ++p)
-        if (p != a.rank) store_sys(reinterpret_cast<float4*>(a.peers[p].ex) + o4 + i, v);
+        if (p != a.rank) store_sys(a.peers[p].ex, (int)(o4 + i), v);
     p2p_stores_done();
 }
 
@@ -107,15 +118,15 @@ __device__ void p2p_push_records(const StepArgs& a) {
 __device__ __forceinline__ void push_row_to(const StepArgs& a, int p, int tab, int row, int lane) {
     const int w = tab ? a.m : a.r;                   // r, m multiples of 4, <= 512
     const float4* s = reinterpret_cast<const float4*>((tab ? a.W : a.A) + (int64_t)row * w);
-    float4* d = reinterpret_cast<float4*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
+    const float* d = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;    // row: wave-uniform
     const int w4 = w / 4;
     float4 v0, v1;
     if (lane < w4) v0 = s[lane];
     if (lane + 64 < w4) v1 = s[lane + 64];
     const float ab = (!tab && lane == 0) ? a.Ab[row] : 0.f;
-    if (lane < w4) store_sys(d + lane, v0);
-    if (lane + 64 < w4) store_sys(d + lane + 64, v1);
-    if (!tab && lane == 0) store_sys(a.peers[p].Ab + row, ab);
+    if (lane < w4) store_sys(d, lane, v0);
+    if (lane + 64 < w4) store_sys(d, lane + 64, v1);
+    if (!tab && lane == 0) store_sys(a.peers[p].Ab, row, ab);
 }
 
 // k_p2p_rows: one wave per (peer, list entry) of batch step_batch(a)'s direction-0 lists (rows
@@ -229,14 +240,14 @@ __device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int ro
     const int w = tab ? a.m : a.r;
     for (int p = 0; p < a.G; ++p) {
         if (!((mk >> p) & 1u)) continue;
-        VT* d = reinterpret_cast<VT*>((tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w);
+        const float* d = (tab ? a.peers[p].W : a.peers[p].A) + (int64_t)row * w;   // row: wave-uniform
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int c = lane + RAE_WAVE * q;
 #if defined(RAE_DIAG) && defined(RAE_PIPE_PLAIN)   // diagnostic A/B only: plain stores
-            if (c < nv) d[c] = v[q];
+            if (c < nv) const_cast<VT*>(reinterpret_cast<const VT*>(d))[c] = v[q];
 #else
-            if (c < nv) store_sys(d + c, v[q]);
+            if (c < nv) store_sys(d, c, v[q]);
 #endif
         }
     }
@@ -244,7 +255,7 @@ __device__ __forceinline__ void pipe_push_row(const StepArgs& a, int tab, int ro
 // ... an entity row's Ab (one lane)
 __device__ __forceinline__ void pipe_push_ab(const StepArgs& a, int row, unsigned mk, float v) {
     for (int p = 0; p < a.G; ++p)
-        if ((mk >> p) & 1u) store_sys(a.peers[p].Ab + row, v);
+        if ((mk >> p) & 1u) store_sys(a.peers[p].Ab, row, v);
 }
 
 // k_p2p_wait: lane p waits for peer p's `per` signals of this step (kind 0 records, 1 rows):

@@ -119,7 +119,7 @@ P2P_PUSHES = ("_Z10k_p2p_rowsN3rae8StepArgsE", "_Z10k_p2p_recsN3rae8StepArgsE",
 
 def _pending_store_at_end(lines):
     """Forward dataflow over the kernel's control-flow graph: is there a path from a
-    global_store to s_endpgm with no `s_waitcnt vmcnt(0)` in between?"""
+    store (global_ / buffer_) to s_endpgm with no `s_waitcnt vmcnt(0)` in between?"""
     addrs = [a for a, _ in lines]
     index = {a: k for k, a in enumerate(addrs)}
     succ = []
@@ -143,7 +143,7 @@ def _pending_store_at_end(lines):
         k = work.pop()
         ins = lines[k][1]
         out = pending[k]
-        if ins.startswith("global_store"):
+        if ins.startswith(("global_store", "buffer_store")):
             out = True
         elif ins.startswith("s_waitcnt") and "vmcnt(0)" in ins:
             out = False
@@ -187,7 +187,7 @@ def test_p2p_pushes_store_write_through_at_system_scope(disasm_addr):
     for name in P2P_PUSHES:
         lines = disasm_addr.get(name)
         assert lines, f"{name} is not in the code object"
-        stores = [c for _, c in lines if c.startswith("global_store")]
+        stores = [c for _, c in lines if c.startswith(("global_store", "buffer_store"))]
         assert stores, name
         for c in stores:
             assert re.search(r"\bsc0\b", c) and re.search(r"\bsc1\b", c), c
