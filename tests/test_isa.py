@@ -192,3 +192,22 @@ def test_p2p_pushes_store_write_through_at_system_scope(disasm_addr):
         for c in stores:
             assert re.search(r"\bsc0\b", c) and re.search(r"\bsc1\b", c), c
         assert not _pending_store_at_end(lines), name
+
+
+def test_no_inline_asm_vector_stores():
+    """Every vector-memory store of the kernels is one the compiler emits (a plain store or a
+    buffer-store builtin), never an inline-asm store: the compiler's hazard and wait-count
+    passes do not see inline asm, and an inline-asm store they cannot see let them reuse or wait
+    wrongly around it (measured: asm `sc1` row stores in the update gave non-finite costs, the
+    same stores as builtins did not -- profiles/r06_ab.txt).  The one inline-asm memory operation
+    kept, the forward's LDS-DMA load, is covered by the M0 tests above."""
+    csrc = os.path.join(ROOT, "relation-autoencoder_amd", "csrc")
+    bad = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".hpp")):
+            continue
+        text = open(os.path.join(csrc, fn)).read()
+        for m in re.finditer(r"asm\s+volatile\s*\((.*?)\)\s*;", text, re.S):
+            if re.search(r"(global|buffer|flat)_store", m.group(1)):
+                bad.append(f"{fn}: {m.group(0)[:80]}")
+    assert not bad, bad
