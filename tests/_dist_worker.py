@@ -239,6 +239,44 @@ def run_gpu(out, decoder, dp_update="replicated", dense="auto", priv="auto", ind
              costs=np.concatenate(ind.epoch_costs), **params)
 
 
+def run_gpu_delay(out, xchg, delay):
+    """a rank that spends host time between single-batch runs (per-batch evaluation,
+    checkpoints) must not make a peer's bounded GPU wait time out.  The peer-to-peer forms with a
+    0.3 s wait bound; rank 1 sleeps `delay` seconds before every batch; run() meets the peers at a
+    host barrier first, so the early rank waits there, not in a wait kernel.  Saves the costs and
+    parameters after `steps` batches (bitwise equal with and without the delay)."""
+    import time
+    from rae import dist as rdist
+    from rae.inducer import ReconstructInducer
+    ws, rk = dist.get_world_size(), dist.get_rank()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    data, gold = _dataset()
+    m, r, s, l = DP_SHAPE["m"], DP_SHAPE["r"], DP_SHAPE["s"], DP_SHAPE["l"]
+    ex = rdist.make_exchange(ws, rk)
+    ind = ReconstructInducer(data, gold, np.random.RandomState(2), 1, 0.1, l, r, m, s, 0.0, 0.0,
+                             "adagrad", "delay", "sp", False, True, False, 1.0, device=dev,
+                             world_size=ws, rank=rk, exchange=ex, graph_chunk=1,
+                             dp_update="partitioned", kernel_forms={"dp_xchg": xchg},
+                             p2p_timeout=0.3)
+    ind.compile_function()
+    eng = ind.engine
+    assert eng.kernel_forms_in_use()["dp_xchg"] == xchg
+    eng.sample_epoch_negatives(ind.negativeSampler, "device")
+    steps = 4
+    for b in range(steps):
+        if rk == 1 and delay > 0:
+            torch.cuda.synchronize()
+            time.sleep(delay)
+        eng.run(b, 1)
+    torch.cuda.synchronize()
+    eng.check()                          # a timed-out wait sets error bit 64: raises here
+    eng.sync_replicas()
+    params = {k: v.detach().cpu().numpy() for k, v in ind.modelFunc.named_params().items()}
+    np.savez(os.path.join(out, f"delay_{xchg}_{delay}_{rk}.npz"),
+             costs=eng.costs[:steps].cpu().numpy(), **params)
+
+
 def run_gpu_c3(out, steps=3, dp_update="replicated", heavy_chunk="auto"):
     """BASELINE config 3 at full size (1M triples) with the global batch of 8 ranks at l=100,
     L = 800, split over 2 ranks of l = 400: the first `steps` batches of an epoch, negatives
@@ -449,6 +487,8 @@ def main():
             run_gpu_c4dp(out, dp_update=dec if dec != "sp" else "replicated")
         elif mode == "gpu_ckpt":
             run_gpu_ckpt(out, dec)
+        elif mode == "gpu_delay":
+            run_gpu_delay(out, dec, float(sys.argv[4]))
         elif mode == "nccl1":
             run_nccl1(out)
         else:

@@ -291,6 +291,22 @@ def test_gpu_c4_shape_data_parallel(built_lib, cuda_dev, tmp_path, ws):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("xchg", ["p2p", "p2p_pipe"])
+def test_gpu_p2p_delayed_rank(built_lib, cuda_dev, tmp_path, xchg):
+    """one rank sleeps 1 s of host time before every single-batch run while the
+    peer-to-peer waits are bounded at 0.3 s (rae_set_p2p_timeout).  run() meets the peers at a
+    host barrier before any wait kernel starts, so no wait times out (error bit 64 would raise in
+    eng.check()), and the costs and parameters equal the undelayed run's bitwise."""
+    _launch(["gpu_delay", str(tmp_path), xchg, "1.0"], nproc=2, timeout=300)
+    _launch(["gpu_delay", str(tmp_path), xchg, "0"], nproc=2, timeout=300)
+    for k in range(2):
+        a = np.load(tmp_path / f"delay_{xchg}_1.0_{k}.npz")
+        b = np.load(tmp_path / f"delay_{xchg}_0.0_{k}.npz")
+        for key in a.files:
+            np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("decoder,ws,graph_chunk,iw,xchg", [
     ("sp", 2, 1, 0, "p2p"), ("sp", 4, 4, 0, "p2p"), ("rescal", 2, 1, 0, "p2p"),
     ("rescal+sp", 4, 1, 0, "p2p"), ("sp", 8, 4, 0, "p2p"), ("sp", 2, 2, 4, "p2p"),
